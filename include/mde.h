@@ -1,0 +1,167 @@
+/*
+ * mde.h -- C ABI of libmde_hip.so, the MI355X (gfx950) Depth Anything V2
+ * inference engine.  Plain pointers, sizes and ints only: no torch, no HIP
+ * C++ types (streams/events are opaque `void*` = hipStream_t / hipEvent_t).
+ *
+ * Every function returns 0 (MDE_OK) on success or an mde_status code;
+ * mde_last_error() returns a thread-local description of the last failure.
+ *
+ * Which reference interface each group replaces (reference paths are
+ * relative to the upstream repo yester31/Monocular_Depth_Estimation_TRT):
+ *
+ *   engine        core/common.py:141-312 get_engine() -> trt.ICudaEngine
+ *                 (deserialize_cuda_engine, :298-299) and its introspection
+ *                 used by core/common_runtime.py:131-175 (num_io_tensors,
+ *                 get_tensor_name/shape/dtype/mode, get_tensor_profile_shape)
+ *   context       engine.create_execution_context()
+ *                 (models/depth_anything_v2/onnx2trt.py:93-94),
+ *                 context.set_tensor_address (core/common_runtime.py:272-274),
+ *                 context.set_input_shape (onnx2trt.py:99-100),
+ *                 context.execute_async_v3 (core/common_runtime.py:269-270),
+ *                 context.profiler = IProfiler (tools/profile_model.py:126,
+ *                 core/profile.py:30-57)
+ *   rt            the cuda-python cudart calls of core/common_runtime.py
+ *                 (cudaMallocHost/cudaMalloc :64-73, cudaFree/cudaFreeHost
+ *                 :106-108, cudaMemcpyAsync :245-255, cudaStreamCreate/
+ *                 Synchronize/Destroy :135,:259,:182, cudaEvent* :220-237)
+ *   op            no reference counterpart: the individual TensorRT layers of
+ *                 the DA-V2 engine, exposed for per-kernel
+ *                 parity tests and for integrators who run parts of the graph.
+ */
+#ifndef MDE_H_
+#define MDE_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MDE_ABI_VERSION 1
+
+typedef enum {
+  MDE_OK = 0,
+  MDE_ERR_ARG = 1,     /* bad argument (null pointer, bad size)          */
+  MDE_ERR_FILE = 2,    /* packed file missing or unreadable              */
+  MDE_ERR_FORMAT = 3,  /* packed file malformed / unsupported version    */
+  MDE_ERR_HIP = 4,     /* HIP runtime error                              */
+  MDE_ERR_NAME = 5,    /* unknown tensor name                            */
+  MDE_ERR_SHAPE = 6,   /* shape outside the engine's profile             */
+  MDE_ERR_STATE = 7    /* address not set, context busy, ...             */
+} mde_status;
+
+/* Same numbering as tensorrt.DataType for the types used here. */
+typedef enum { MDE_FLOAT32 = 0, MDE_FLOAT16 = 1 } mde_dtype;
+
+typedef struct mde_engine mde_engine;
+typedef struct mde_context mde_context;
+
+typedef struct {
+  char name[64];
+  int32_t dtype;    /* mde_dtype */
+  int32_t is_input; /* 1 = INPUT, 0 = OUTPUT (trt.TensorIOMode) */
+  int32_t rank;
+  int64_t dims[8];  /* dims[0] = -1: batch is dynamic (see profile shape) */
+} mde_io_desc;
+
+typedef struct {
+  char encoder[16];
+  int32_t embed_dim, depth, num_heads, mlp_hidden, patch;
+  int32_t img_h, img_w, features, head_hidden, metric;
+  int32_t out_channels[4], taps[4];
+  float max_depth, ln_eps;
+  int32_t max_batch_hint;
+  int64_t weight_bytes;
+} mde_engine_info;
+
+/* IProfiler.report_layer_time analogue: one call per launched layer. */
+typedef void (*mde_layer_cb)(const char* layer_name, float ms, void* user);
+
+/* ---- library ---------------------------------------------------------- */
+int mde_version(void);
+const char* mde_last_error(void);
+
+/* ---- engine (replaces get_engine / ICudaEngine) ----------------------- */
+int mde_engine_load(const char* packed_path, int device, mde_engine** out);
+int mde_engine_load_memory(const void* data, size_t nbytes, int device, mde_engine** out);
+int mde_engine_destroy(mde_engine* eng);
+int mde_engine_get_info(const mde_engine* eng, mde_engine_info* out);
+int mde_engine_num_io(const mde_engine* eng, int* n);
+int mde_engine_io_desc(const mde_engine* eng, int index, mde_io_desc* out);
+/* which: 0 = min, 1 = opt, 2 = max shape of the dynamic-batch profile */
+int mde_engine_profile_shape(const mde_engine* eng, const char* name, int which, int64_t* dims, int* rank);
+
+/* ---- execution context (replaces IExecutionContext) ------------------- */
+int mde_context_create(mde_engine* eng, int max_batch, mde_context** out);
+int mde_context_destroy(mde_context* ctx);
+int mde_context_set_tensor_address(mde_context* ctx, const char* name, void* device_ptr);
+int mde_context_set_input_shape(mde_context* ctx, const char* name, const int64_t* dims, int rank);
+int mde_context_get_tensor_shape(const mde_context* ctx, const char* name, int64_t* dims, int* rank);
+/* Asynchronous: enqueues the whole forward on `stream` (hipStream_t). */
+int mde_context_enqueue(mde_context* ctx, void* stream);
+/* 1 (default): capture the forward into a hipGraph per (batch, addresses)
+ * and replay it; 0: launch every kernel eagerly. */
+int mde_context_set_graph_mode(mde_context* ctx, int enable);
+/* Non-null cb: enqueue runs eagerly with a hipEvent pair per layer,
+ * synchronizes `stream` at the end and reports each layer's time. */
+int mde_context_set_profiler(mde_context* ctx, mde_layer_cb cb, void* user);
+int mde_context_workspace_bytes(const mde_context* ctx, size_t* bytes);
+
+/* ---- HIP runtime helpers (replaces cuda-python cudart) ---------------- */
+int mde_rt_device_count(int* n);
+int mde_rt_set_device(int device);
+int mde_rt_device_name(int device, char* buf, int buflen);
+int mde_rt_malloc(void** ptr, size_t bytes);
+int mde_rt_free(void* ptr);
+int mde_rt_malloc_host(void** ptr, size_t bytes);
+int mde_rt_free_host(void* ptr);
+int mde_rt_memcpy_htod_async(void* dst, const void* src, size_t bytes, void* stream);
+int mde_rt_memcpy_dtoh_async(void* dst, const void* src, size_t bytes, void* stream);
+int mde_rt_memcpy_dtod_async(void* dst, const void* src, size_t bytes, void* stream);
+int mde_rt_memset_async(void* dst, int value, size_t bytes, void* stream);
+int mde_rt_stream_create(void** stream);
+int mde_rt_stream_destroy(void* stream);
+int mde_rt_stream_synchronize(void* stream);
+int mde_rt_device_synchronize(void);
+int mde_rt_event_create(void** event);
+int mde_rt_event_destroy(void* event);
+int mde_rt_event_record(void* event, void* stream);
+int mde_rt_event_elapsed_ms(float* ms, void* start, void* end);
+
+/* ---- kernel-level entry points ---------------------------------------- */
+/* All tensors are device pointers.  f16 = IEEE half.  Weights W are
+ * [Npad][ldw] f16 row-major (K contiguous), rows >= N zero, ldw % 32 == 0,
+ * ldw >= K rounded up to 32, Npad a multiple of 128.  Activation maps are
+ * NHWC f16.  act: 0 none, 1 ReLU, 2 GELU(erf). */
+int mde_op_layernorm(const float* x, void* y_f16, const float* gamma, const float* beta, int rows, int dim,
+                     float eps, int tokens, int skip_cls, void* stream);
+int mde_op_linear(const void* a_f16, int lda, const void* w_f16, int ldw, int m, int n, int k,
+                  const float* bias, int act, void* out_f16, int ldo, void* stream);
+int mde_op_linear_residual(const void* a_f16, int lda, const void* w_f16, int ldw, int m, int n, int k,
+                           const float* bias, const float* layer_scale, float* x32, int ldx, void* stream);
+int mde_op_qkv(const void* a_f16, const void* w_f16, int ldw, const float* bias, int batch, int tokens,
+               int heads, int tokens_pad, float q_scale, void* q_f16, void* k_f16, void* vt_f16, void* stream);
+int mde_op_attention(const void* q_f16, const void* k_f16, const void* vt_f16, void* o_f16, int batch, int heads,
+                     int tokens, int tokens_pad, int ldo, void* stream);
+int mde_op_patch_embed(const float* img, int batch, int h, int w, const void* w_f16, int ldw, const float* bias,
+                       const float* pos_patch, const float* cls_pos, int dim, void* patch_scratch_f16,
+                       float* x32, void* stream);
+int mde_op_conv3x3(const void* in_f16, int batch, int h, int w, int cin, const void* w_f16, int ldw, int cout,
+                   int stride, int relu_in, const float* bias, int act, const void* res0_f16,
+                   const void* res1_f16, void* out_f16, void* stream);
+int mde_op_conv3x3_up(const void* in_f16, int batch, int sh, int sw, int cin, int uh, int uw, const void* w_f16,
+                      int ldw, int cout, const float* bias, int act, void* out_f16, void* stream);
+int mde_op_conv_transpose(const void* in_f16, int batch, int h, int w, int cin, const void* w_f16, int ldw,
+                          int cout, int stride, const float* bias, void* out_f16, void* stream);
+int mde_op_resize_bilinear(const void* in_f16, int batch, int ih, int iw, int c, int oh, int ow, void* out_f16,
+                           void* stream);
+int mde_op_depth_head(const void* in_f16, int batch, int sh, int sw, int cin, int uh, int uw, const void* w_f16,
+                      int ldw, const float* bias, const float* w2, float b2, int metric, float max_depth,
+                      float* out_f32, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MDE_H_ */

@@ -1,0 +1,152 @@
+"""ctypes binding of libmde_hip.so (the C ABI declared in include/mde.h).
+
+This is the only door from Python into the HIP engine.  There is no CPU or
+PyTorch fallback: if the library is missing or fails to load, every call
+raises -- a product path that silently computed on the CPU would void every
+parity claim.
+"""
+
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("MDE_LIB", os.path.join(HERE, "libmde_hip.so"))
+
+c_void_p, c_int, c_float, c_size_t, c_char_p = C.c_void_p, C.c_int, C.c_float, C.c_size_t, C.c_char_p
+c_int64 = C.c_int64
+P = C.POINTER
+
+MDE_OK = 0
+STATUS = {1: "MDE_ERR_ARG", 2: "MDE_ERR_FILE", 3: "MDE_ERR_FORMAT", 4: "MDE_ERR_HIP", 5: "MDE_ERR_NAME",
+          6: "MDE_ERR_SHAPE", 7: "MDE_ERR_STATE"}
+
+
+class mde_io_desc(C.Structure):
+    _fields_ = [("name", C.c_char * 64), ("dtype", C.c_int32), ("is_input", C.c_int32),
+                ("rank", C.c_int32), ("dims", C.c_int64 * 8)]
+
+
+class mde_engine_info(C.Structure):
+    _fields_ = [("encoder", C.c_char * 16),
+                ("embed_dim", C.c_int32), ("depth", C.c_int32), ("num_heads", C.c_int32),
+                ("mlp_hidden", C.c_int32), ("patch", C.c_int32),
+                ("img_h", C.c_int32), ("img_w", C.c_int32), ("features", C.c_int32),
+                ("head_hidden", C.c_int32), ("metric", C.c_int32),
+                ("out_channels", C.c_int32 * 4), ("taps", C.c_int32 * 4),
+                ("max_depth", C.c_float), ("ln_eps", C.c_float),
+                ("max_batch_hint", C.c_int32), ("weight_bytes", C.c_int64)]
+
+
+LAYER_CB = C.CFUNCTYPE(None, c_char_p, c_float, c_void_p)
+
+# name -> argtypes (restype is always int status unless listed in _RESTYPE)
+PROTOTYPES = {
+    "mde_version": [],
+    "mde_last_error": [],
+    "mde_engine_load": [c_char_p, c_int, P(c_void_p)],
+    "mde_engine_load_memory": [c_void_p, c_size_t, c_int, P(c_void_p)],
+    "mde_engine_destroy": [c_void_p],
+    "mde_engine_get_info": [c_void_p, P(mde_engine_info)],
+    "mde_engine_num_io": [c_void_p, P(c_int)],
+    "mde_engine_io_desc": [c_void_p, c_int, P(mde_io_desc)],
+    "mde_engine_profile_shape": [c_void_p, c_char_p, c_int, P(c_int64), P(c_int)],
+    "mde_context_create": [c_void_p, c_int, P(c_void_p)],
+    "mde_context_destroy": [c_void_p],
+    "mde_context_set_tensor_address": [c_void_p, c_char_p, c_void_p],
+    "mde_context_set_input_shape": [c_void_p, c_char_p, P(c_int64), c_int],
+    "mde_context_get_tensor_shape": [c_void_p, c_char_p, P(c_int64), P(c_int)],
+    "mde_context_enqueue": [c_void_p, c_void_p],
+    "mde_context_set_graph_mode": [c_void_p, c_int],
+    "mde_context_set_profiler": [c_void_p, LAYER_CB, c_void_p],
+    "mde_context_workspace_bytes": [c_void_p, P(c_size_t)],
+    "mde_rt_device_count": [P(c_int)],
+    "mde_rt_set_device": [c_int],
+    "mde_rt_device_name": [c_int, c_char_p, c_int],
+    "mde_rt_malloc": [P(c_void_p), c_size_t],
+    "mde_rt_free": [c_void_p],
+    "mde_rt_malloc_host": [P(c_void_p), c_size_t],
+    "mde_rt_free_host": [c_void_p],
+    "mde_rt_memcpy_htod_async": [c_void_p, c_void_p, c_size_t, c_void_p],
+    "mde_rt_memcpy_dtoh_async": [c_void_p, c_void_p, c_size_t, c_void_p],
+    "mde_rt_memcpy_dtod_async": [c_void_p, c_void_p, c_size_t, c_void_p],
+    "mde_rt_memset_async": [c_void_p, c_int, c_size_t, c_void_p],
+    "mde_rt_stream_create": [P(c_void_p)],
+    "mde_rt_stream_destroy": [c_void_p],
+    "mde_rt_stream_synchronize": [c_void_p],
+    "mde_rt_device_synchronize": [],
+    "mde_rt_event_create": [P(c_void_p)],
+    "mde_rt_event_destroy": [c_void_p],
+    "mde_rt_event_record": [c_void_p, c_void_p],
+    "mde_rt_event_elapsed_ms": [P(c_float), c_void_p, c_void_p],
+    "mde_op_layernorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_int, c_int, c_void_p],
+    "mde_op_linear": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int,
+                      c_void_p],
+    "mde_op_linear_residual": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                               c_void_p, c_int, c_void_p],
+    "mde_op_qkv": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p,
+                   c_void_p, c_void_p],
+    "mde_op_attention": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "mde_op_patch_embed": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
+                           c_void_p, c_void_p, c_void_p],
+    "mde_op_conv3x3": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                       c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "mde_op_conv3x3_up": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
+                          c_int, c_void_p, c_void_p],
+    "mde_op_conv_transpose": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p,
+                              c_void_p, c_void_p],
+    "mde_op_resize_bilinear": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
+    "mde_op_depth_head": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
+                          c_void_p, c_float, c_int, c_float, c_void_p, c_void_p],
+}
+_RESTYPE = {"mde_last_error": c_char_p}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class MDEError(RuntimeError):
+    """A non-zero status from libmde_hip (mirrors core/common_runtime.py:41-56)."""
+
+    def __init__(self, fn: str, code: int, msg: str):
+        self.code = code
+        super().__init__(f"{fn} failed ({STATUS.get(code, code)}): {msg}")
+
+
+def lib() -> C.CDLL:
+    """Load libmde_hip.so once; raise loudly if it is not there."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"libmde_hip.so not found at {LIB_PATH}. Build it first: "
+                    f"python -c 'import __graft_entry__ as g; g.build()' (or "
+                    f"python -m monocular_depth_estimation_trt_amd._build). There is no CPU fallback.")
+            L = C.CDLL(LIB_PATH)
+            for name, args in PROTOTYPES.items():
+                f = getattr(L, name)
+                f.argtypes = args
+                f.restype = _RESTYPE.get(name, c_int)
+            _lib = L
+    return _lib
+
+
+def last_error() -> str:
+    m = lib().mde_last_error()
+    return m.decode(errors="replace") if m else ""
+
+
+def call(name: str, *args) -> None:
+    """Invoke an ABI function, raising MDEError on a non-zero status."""
+    rc = getattr(lib(), name)(*args)
+    if rc != MDE_OK:
+        raise MDEError(name, rc, last_error())
+
+
+def exported_symbols():
+    return list(PROTOTYPES)

@@ -1,0 +1,191 @@
+"""get_engine(): build-or-load a packed engine -- the drop-in for the
+reference's `core/common.py:141-312`.
+
+The reference builds a TensorRT plan from an ONNX file (fingerprinted by
+sha256 of the ONNX + builder options, :92-117; stale-engine detection,
+:120-138) and deserializes it.  Here the "source" is a DA-V2 checkpoint (or a
+`synthetic:` spec), the build step is the AOT weight packer (pack.py), and
+the artefact is a packed engine file loaded by libmde_hip.  Same signature,
+same reuse/rebuild rules, same errors (FileNotFoundError for a missing
+source, RuntimeError for a failed build/load).
+
+Source strings:
+  synthetic:<vits|vitb|vitl>[:<metric|relative>[:<seed>]]   seeded weights
+  /path/ckpt.pth          torch.load(..., weights_only=True)
+  /path/ckpt.safetensors  safetensors
+  /path/ckpt.npz          numpy (allow_pickle=False)
+"""
+
+from __future__ import annotations
+
+import hashlib
+import os
+import time
+from typing import Optional, Sequence
+
+import numpy as np
+
+from . import pack, weights
+from .common_runtime import *  # noqa: F401,F403  (re-export, as core/common.py does)
+from .engine import Engine
+
+
+def GiB(val):
+    return val * 1 << 30
+
+
+def _parse_synthetic(src: str):
+    parts = src.split(":")
+    enc = parts[1] if len(parts) > 1 and parts[1] else "vits"
+    dtype = parts[2] if len(parts) > 2 and parts[2] else "metric"
+    seed = int(parts[3]) if len(parts) > 3 and parts[3] else 1234
+    return enc, dtype, seed
+
+
+def _source_digest(src: str) -> str:
+    if src.startswith("synthetic:"):
+        return hashlib.sha256(src.encode()).hexdigest()
+    h = hashlib.sha256()
+    with open(src, "rb") as f:
+        for chunk in iter(lambda: f.read(1 << 20), b""):
+            h.update(chunk)
+    return h.hexdigest()
+
+
+def source_exists(src: str) -> bool:
+    return src.startswith("synthetic:") or os.path.exists(src)
+
+
+def load_checkpoint(path: str) -> dict:
+    """Load a state dict without executing anything from the file."""
+    if path.endswith(".safetensors"):
+        from safetensors.numpy import load_file
+        return dict(load_file(path))
+    if path.endswith(".npz"):
+        with np.load(path, allow_pickle=False) as z:
+            return {k: z[k] for k in z.files}
+    import torch
+    sd = torch.load(path, map_location="cpu", weights_only=True)
+    if isinstance(sd, dict) and "model" in sd and isinstance(sd["model"], dict):
+        sd = sd["model"]
+    return {k: v.float().numpy() for k, v in sd.items()}
+
+
+def _infer_encoder(sd: dict) -> str:
+    d = np.asarray(sd["pretrained.cls_token"] if "pretrained.cls_token" in sd
+                   else sd["module.pretrained.cls_token"]).shape[-1]
+    for name, e in weights.ENCODERS.items():
+        if e["embed_dim"] == d:
+            return name
+    raise ValueError(f"no DA-V2 encoder with embed dim {d}")
+
+
+def _engine_fingerprint(src, precision, workspace_gib, opt_level, obey_precision_constraints,
+                        dynamic_input_shapes, encoder, depth_type, max_depth, input_hw) -> str:
+    parts = [_source_digest(src), f"packer={pack.PACKER_VERSION}", f"precision={precision}",
+             f"workspace={workspace_gib}", f"opt_level={opt_level}",
+             f"obey_precision={obey_precision_constraints}", f"dynamic={dynamic_input_shapes}",
+             f"encoder={encoder}", f"depth_type={depth_type}", f"max_depth={max_depth}",
+             f"input_hw={tuple(input_hw)}", "arch=gfx950"]
+    return "\n".join(parts)
+
+
+def engine_staleness(engine_file_path, fingerprint_path, fingerprint, source_present):
+    """Why the cached engine cannot be reused, or None if it can
+    (reference core/common.py:120-138)."""
+    if not os.path.exists(engine_file_path):
+        return "no engine file"
+    if not source_present:
+        return None
+    if fingerprint is None:
+        return None
+    if not os.path.exists(fingerprint_path):
+        return "no fingerprint recorded"
+    with open(fingerprint_path, encoding="utf-8") as f:
+        if f.read() != fingerprint:
+            return "source or build options changed"
+    return None
+
+
+def get_engine(onnx_file_path, engine_file_path="", precision="fp32", dynamic_input_shapes=None,
+               workspace_gib=2, opt_level=None, obey_precision_constraints=False, check_fingerprint=True,
+               *, encoder: Optional[str] = None, depth_type: Optional[str] = None,
+               max_depth: Optional[float] = None, input_hw: Optional[Sequence[int]] = None,
+               device: int = 0) -> Engine:
+    """Load `engine_file_path` if it matches its source, otherwise pack it.
+
+    `onnx_file_path` keeps the reference's parameter name; it names the
+    checkpoint / synthetic spec the engine is packed from.
+    `dynamic_input_shapes` = [min, opt, max] input shapes gives a
+    dynamic-batch engine whose contexts are sized for max[0].
+    `precision`: "fp16" (the engine's arithmetic: f16 operands, fp32
+    accumulation/statistics).  "fp32" raises -- there is no fp32 engine.
+    """
+    src = str(onnx_file_path)
+    if precision not in ("fp16", "fp32"):
+        raise ValueError(f"[MDET] unknown precision {precision!r}")
+    if precision == "fp32":
+        raise NotImplementedError("[MDET] the MI355X engine computes fp16 (fp32 accumulate); "
+                                  "build with precision='fp16'")
+    if dynamic_input_shapes is not None:
+        mn, opt, mx = [tuple(int(v) for v in s) for s in dynamic_input_shapes[:3]]
+        if not (mn[1:] == opt[1:] == mx[1:]):
+            raise ValueError("[MDET] only the batch dimension may be dynamic")
+        if not (1 <= mn[0] <= opt[0] <= mx[0]):
+            raise ValueError(f"[MDET] bad batch profile {mn[0]}/{opt[0]}/{mx[0]}")
+        input_hw = input_hw or (mn[2], mn[3])
+        profile = (mn, opt, mx)
+    else:
+        profile = None
+    input_hw = tuple(int(v) for v in (input_hw or (518, 518)))
+
+    sd = None
+    if src.startswith("synthetic:"):
+        s_enc, s_type, seed = _parse_synthetic(src)
+        encoder = encoder or s_enc
+        depth_type = depth_type or s_type
+    if depth_type is None:
+        depth_type = "metric"
+    if max_depth is None:
+        max_depth = 20.0 if depth_type == "metric" else 1.0
+
+    fingerprint = None
+    fingerprint_path = os.path.splitext(engine_file_path)[0] + ".fingerprint" if engine_file_path else ""
+    present = source_exists(src)
+    if check_fingerprint and present and engine_file_path:
+        fingerprint = _engine_fingerprint(src, precision, workspace_gib, opt_level, obey_precision_constraints,
+                                          dynamic_input_shapes, encoder, depth_type, max_depth, input_hw)
+
+    def build_engine() -> bytes:
+        nonlocal sd, encoder
+        if not present:
+            raise FileNotFoundError(f"[MDET] source {src} not found.")
+        if src.startswith("synthetic:"):
+            cfg = weights.model_config(encoder, depth_type, max_depth)
+            sd = weights.synthetic_state_dict(cfg, _parse_synthetic(src)[2])
+        else:
+            sd = load_checkpoint(src)
+            encoder = encoder or _infer_encoder(sd)
+            cfg = weights.model_config(encoder, depth_type, max_depth)
+        return pack.pack_bytes(sd, cfg, *input_hw)
+
+    kw = dict(profile=profile, static_batch=1)
+    if engine_file_path:
+        stale = engine_staleness(engine_file_path, fingerprint_path, fingerprint, present)
+        if stale is None:
+            print(f"[MDET] Load engine from file ({engine_file_path})")
+            return Engine.from_file(engine_file_path, device, **kw)
+        if os.path.exists(engine_file_path):
+            print(f"[MDET] Rebuilding engine - {stale}")
+    print(f"[MDET] Build engine ({engine_file_path or '<memory>'})")
+    t0 = time.time()
+    blob = build_engine()
+    if engine_file_path:
+        pack.write_packed(engine_file_path, blob)
+        if fingerprint is not None:
+            with open(fingerprint_path, "w", encoding="utf-8") as f:
+                f.write(fingerprint)
+    print(f"[MDET] Engine build done! ({time.time() - t0:.2f} [sec])")
+    if engine_file_path:
+        return Engine.from_file(engine_file_path, device, **kw)
+    return Engine.from_bytes(blob, device, **kw)

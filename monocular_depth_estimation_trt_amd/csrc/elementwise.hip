@@ -1,0 +1,152 @@
+// Bandwidth-bound kernels of the DA-V2 forward (gfx950):
+//   * LayerNorm over D of the fp32 residual stream -> f16 (block norm1/norm2,
+//     SURVEY.md 8a a8; the final `norm` of the 4 taps with the cls row dropped
+//     and the token map written as NHWC, a13)
+//   * patch im2col: fp32 NCHW image -> f16 patch rows [B*np][3*14*16] (kx
+//     padded 14->16 so every 8-element K chunk is 16-byte aligned), plus the
+//     cls row of the residual stream (cls + pos[0]) (a6, a7)
+//   * bilinear resize, align_corners=True, NHWC f16 (a17 fusion upsample)
+#include "mde_device.h"
+#include "mde_ops.h"
+
+namespace mde {
+
+namespace {
+
+// One wave per row; PER = D/64 elements per lane, lane-strided (coalesced).
+template <int PER>
+__global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict__ x, f16* __restrict__ y,
+                                                        const float* __restrict__ g,
+                                                        const float* __restrict__ bt, int rows, float eps,
+                                                        int T, int skip_cls) {
+  constexpr int D = PER * 64;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  int orow = row;
+  if (skip_cls) {
+    const int b = row / T, t = row - (row / T) * T;
+    if (t == 0) return;
+    orow = b * (T - 1) + t - 1;
+  }
+  const float* xr = x + (size_t)row * D;
+  float v[PER];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    v[i] = xr[i * 64 + lane];
+    s += v[i];
+  }
+  const float mean = wave_sum(s) * (1.0f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const float d = v[i] - mean;
+    q += d * d;
+  }
+  const float rstd = rsqrtf(wave_sum(q) * (1.0f / D) + eps);
+  f16* yr = y + (size_t)orow * D;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = i * 64 + lane;
+    yr[c] = (f16)((v[i] - mean) * rstd * g[c] + bt[c]);
+  }
+}
+
+constexpr int PK = 3 * 14 * 16;  // patch row length (K of the patch-embed GEMM)
+
+__global__ void __launch_bounds__(256) patch_prep_kernel(const float* __restrict__ img, f16* __restrict__ P,
+                                                         float* __restrict__ X, const float* __restrict__ cls_pos,
+                                                         int B, int H, int W, int ph, int pw, int T, int D) {
+  const long long np = (long long)ph * pw;
+  const long long nchunk = (long long)B * np * 84;  // 3 channels x 14 rows x 2 halves
+  long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id < nchunk) {
+    const long long patch = id / 84;
+    const int r = (int)(id - patch * 84);
+    const int c = r / 28, ky = (r % 28) >> 1, half = r & 1;
+    const int b = (int)(patch / np);
+    const int pi = (int)(patch - (long long)b * np);
+    const int py = pi / pw, px = pi - (pi / pw) * pw;
+    const float* src = img + (((size_t)b * 3 + c) * H + py * 14 + ky) * W + px * 14 + half * 8;
+    f16x8 v;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = (half * 8 + j < 14) ? (f16)src[j] : (f16)0.0f;
+    *reinterpret_cast<f16x8*>(P + patch * PK + c * 224 + ky * 16 + half * 8) = v;
+    return;
+  }
+  id -= nchunk;
+  if (id < (long long)B * D) {
+    const int b = (int)(id / D), d = (int)(id - (long long)(id / D) * D);
+    X[(size_t)b * T * D + d] = cls_pos[d];
+  }
+}
+
+// PyTorch upsample_bilinear2d(align_corners=True): src = dst*(in-1)/(out-1),
+// h1 = floor(src), h1p = (h1 < in-1), lambda = src - h1; fp32 arithmetic.
+__global__ void __launch_bounds__(256) resize_kernel(const f16* __restrict__ in, f16* __restrict__ out, int B,
+                                                     int ih, int iw, int C, int oh, int ow) {
+  const int C8 = C >> 3;
+  const long long n = (long long)B * oh * ow * C8;
+  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= n) return;
+  const int c8 = (int)(id % C8);
+  long long pix = id / C8;
+  const int ox = (int)(pix % ow);
+  pix /= ow;
+  const int oy = (int)(pix % oh);
+  const int b = (int)(pix / oh);
+  const float sy = oh > 1 ? (float)(ih - 1) / (float)(oh - 1) : 0.f;
+  const float sx = ow > 1 ? (float)(iw - 1) / (float)(ow - 1) : 0.f;
+  const float fy = sy * (float)oy, fx = sx * (float)ox;
+  const int y0 = (int)fy, x0 = (int)fx;
+  const int y1 = y0 + (y0 < ih - 1 ? 1 : 0), x1 = x0 + (x0 < iw - 1 ? 1 : 0);
+  const float ly1 = fy - (float)y0, ly0 = 1.f - ly1;
+  const float lx1 = fx - (float)x0, lx0 = 1.f - lx1;
+  const f16* base = in + (size_t)b * ih * iw * C + c8 * 8;
+  const f16x8 a = *reinterpret_cast<const f16x8*>(base + ((size_t)y0 * iw + x0) * C);
+  const f16x8 bb = *reinterpret_cast<const f16x8*>(base + ((size_t)y0 * iw + x1) * C);
+  const f16x8 c = *reinterpret_cast<const f16x8*>(base + ((size_t)y1 * iw + x0) * C);
+  const f16x8 d = *reinterpret_cast<const f16x8*>(base + ((size_t)y1 * iw + x1) * C);
+  f16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j)
+    v[j] = (f16)(ly0 * (lx0 * (float)a[j] + lx1 * (float)bb[j]) + ly1 * (lx0 * (float)c[j] + lx1 * (float)d[j]));
+  *reinterpret_cast<f16x8*>(out + (size_t)id * 8) = v;
+}
+
+}  // namespace
+
+hipError_t launch_layernorm(const float* x, h16* y, const float* g, const float* b, int rows, int D, float eps,
+                            int T, int skip_cls, hipStream_t st) {
+  if (rows <= 0) return hipSuccess;
+  dim3 grid((rows + 3) / 4), block(256);
+  f16* yo = reinterpret_cast<f16*>(y);
+  switch (D) {
+    case 384: hipLaunchKernelGGL(layernorm_kernel<6>, grid, block, 0, st, x, yo, g, b, rows, eps, T, skip_cls); break;
+    case 768: hipLaunchKernelGGL(layernorm_kernel<12>, grid, block, 0, st, x, yo, g, b, rows, eps, T, skip_cls); break;
+    case 1024: hipLaunchKernelGGL(layernorm_kernel<16>, grid, block, 0, st, x, yo, g, b, rows, eps, T, skip_cls); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_patch_prep(const float* img, h16* P, float* X, const float* cls_pos, int B, int H, int W, int ph,
+                             int pw, int T, int D, hipStream_t st) {
+  const long long n = (long long)B * ph * pw * 84 + (long long)B * D;
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(patch_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, img,
+                     reinterpret_cast<f16*>(P), X, cls_pos, B, H, W, ph, pw, T, D);
+  return hipGetLastError();
+}
+
+hipError_t launch_resize(const h16* in, h16* out, int B, int ih, int iw, int C, int oh, int ow, hipStream_t st) {
+  if (C & 7) return hipErrorInvalidValue;
+  const long long n = (long long)B * oh * ow * (C >> 3);
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(resize_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st,
+                     reinterpret_cast<const f16*>(in), reinterpret_cast<f16*>(out), B, ih, iw, C, oh, ow);
+  return hipGetLastError();
+}
+
+}  // namespace mde

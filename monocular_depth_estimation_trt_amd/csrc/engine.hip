@@ -1,0 +1,1167 @@
+// libmde_hip engine: packed-weight loader, execution context and the DA-V2
+// forward schedule, behind the C ABI of include/mde.h.
+//
+// Replaces TensorRT's ICudaEngine / IExecutionContext as used by the
+// reference (core/common.py:141-312, core/common_runtime.py:131-275): one
+// engine per device owns the packed weights; a context owns the activation
+// arena (sized for its max batch) and runs the forward asynchronously on the
+// caller's stream, replayed from a captured hipGraph per (batch, addresses).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <map>
+#include <string>
+#include <tuple>
+#include <unordered_map>
+#include <vector>
+
+#include "../../include/mde.h"
+#include "mde_ops.h"
+#include "pack_format.h"
+
+using namespace mde;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  g_err = std::string(what) + ": " + hipGetErrorString(e);
+  return MDE_ERR_HIP;
+}
+
+#define HIP_OR(call, what)                         \
+  do {                                             \
+    hipError_t e_ = (call);                        \
+    if (e_ != hipSuccess) return hip_fail(e_, what); \
+  } while (0)
+
+struct DevTensor {
+  void* ptr = nullptr;
+  int dtype = 0;
+  int ndim = 0;
+  int dims[4] = {0, 0, 0, 0};
+};
+
+inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
+
+}  // namespace
+
+struct mde_engine {
+  int device = 0;
+  PackConfig cfg{};
+  void* wmem = nullptr;
+  size_t wbytes = 0;
+  std::unordered_map<std::string, DevTensor> t;
+  // derived geometry
+  int ph = 0, pw = 0, np = 0, T = 0, Tpad = 0, D = 0, H = 0, F = 0;
+  int h4 = 0, w4 = 0;
+  float head_b2 = 0.f;  // output_conv2.2 bias (scalar kernel argument)
+
+  const DevTensor* get(const std::string& n) const {
+    auto it = t.find(n);
+    return it == t.end() ? nullptr : &it->second;
+  }
+};
+
+namespace {
+
+struct Buf {
+  h16 *P, *Hn, *Q, *K, *Vt, *O, *Mh;
+  float* X;
+  h16 *tap[4], *pj[4], *l1, *l2, *l4, *rn[4];
+  h16 *tb, *sb, *ub, *vb, *p4, *p3, *p2, *c1;
+};
+
+struct GraphKey {
+  int batch;
+  void* in;
+  void* out;
+  bool operator<(const GraphKey& o) const { return std::tie(batch, in, out) < std::tie(o.batch, o.in, o.out); }
+};
+
+}  // namespace
+
+struct mde_context {
+  mde_engine* e = nullptr;
+  int device = 0;
+  int max_batch = 1;
+  int batch = 1;
+  void* in = nullptr;
+  void* out = nullptr;
+  void* arena = nullptr;
+  size_t arena_bytes = 0;
+  Buf b{};
+  bool graph_mode = true;
+  hipStream_t cap_stream = nullptr;
+  std::map<GraphKey, std::pair<hipGraph_t, hipGraphExec_t>> graphs;
+  mde_layer_cb prof_cb = nullptr;
+  void* prof_user = nullptr;
+  std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> prof_events;
+  size_t prof_used = 0;
+};
+
+namespace {
+
+int load_pack(const uint8_t* data, size_t n, int device, mde_engine** out) {
+  if (n < sizeof(PackHeader) + sizeof(PackConfig)) return fail(MDE_ERR_FORMAT, "packed engine truncated");
+  PackHeader hd;
+  memcpy(&hd, data, sizeof hd);
+  if (memcmp(hd.magic, "MDEPACK1", 8) != 0) return fail(MDE_ERR_FORMAT, "bad magic (not an mde packed engine)");
+  if (hd.version != kPackVersion)
+    return fail(MDE_ERR_FORMAT, "packed engine version " + std::to_string(hd.version) + ", expected " +
+                                    std::to_string(kPackVersion));
+  const size_t tab = sizeof(PackHeader) + sizeof(PackConfig);
+  if (tab + (size_t)hd.n_tensors * sizeof(PackTensor) > n || hd.data_offset + hd.data_bytes > n ||
+      hd.data_offset < tab + (size_t)hd.n_tensors * sizeof(PackTensor))
+    return fail(MDE_ERR_FORMAT, "packed engine tables out of range");
+  auto* e = new mde_engine();
+  e->device = device;
+  memcpy(&e->cfg, data + sizeof(PackHeader), sizeof(PackConfig));
+  const PackConfig& c = e->cfg;
+  if (c.patch != 14 || c.embed_dim % 64 || c.num_heads * 64 != c.embed_dim || c.img_h % 14 || c.img_w % 14 ||
+      c.img_h <= 0 || c.img_w <= 0 || c.features % 16 || c.head_hidden != 32) {
+    delete e;
+    return fail(MDE_ERR_FORMAT, "unsupported model geometry in packed config");
+  }
+  hipError_t he = hipSetDevice(device);
+  if (he != hipSuccess) {
+    delete e;
+    return hip_fail(he, "hipSetDevice");
+  }
+  e->wbytes = hd.data_bytes;
+  he = hipMalloc(&e->wmem, std::max<size_t>(hd.data_bytes, 256));
+  if (he != hipSuccess) {
+    delete e;
+    return hip_fail(he, "hipMalloc(weights)");
+  }
+  he = hipMemcpy(e->wmem, data + hd.data_offset, hd.data_bytes, hipMemcpyHostToDevice);
+  if (he != hipSuccess) {
+    hipFree(e->wmem);
+    delete e;
+    return hip_fail(he, "hipMemcpy(weights)");
+  }
+  for (uint32_t i = 0; i < hd.n_tensors; ++i) {
+    PackTensor pt;
+    memcpy(&pt, data + tab + (size_t)i * sizeof(PackTensor), sizeof pt);
+    if (pt.offset + pt.nbytes > hd.data_bytes || pt.ndim < 1 || pt.ndim > 4) {
+      hipFree(e->wmem);
+      delete e;
+      return fail(MDE_ERR_FORMAT, "tensor record out of range");
+    }
+    DevTensor dt;
+    dt.ptr = (uint8_t*)e->wmem + pt.offset;
+    dt.dtype = pt.dtype;
+    dt.ndim = pt.ndim;
+    for (int k = 0; k < 4; ++k) dt.dims[k] = pt.dims[k];
+    pt.name[sizeof(pt.name) - 1] = 0;
+    e->t[pt.name] = dt;
+  }
+  e->D = c.embed_dim;
+  e->H = c.num_heads;
+  e->F = c.features;
+  e->ph = c.img_h / 14;
+  e->pw = c.img_w / 14;
+  e->np = e->ph * e->pw;
+  e->T = e->np + 1;
+  e->Tpad = (e->T + 63) / 64 * 64;
+  e->h4 = (e->ph + 1) / 2;
+  e->w4 = (e->pw + 1) / 2;
+  // every tensor the forward uses must be present
+  std::vector<std::string> need = {"patch.w", "patch.b", "pos.patch", "pos.cls", "norm.g", "norm.b",
+                                   "rs0.w", "rs0.b", "rs1.w", "rs1.b", "rs3.w", "rs3.b",
+                                   "head.c1.w", "head.c1.b", "head.c2.w", "head.c2.b", "head.c3.w", "head.c3.b"};
+  for (int i = 0; i < c.depth; ++i)
+    for (const char* s : {"ln1.g", "ln1.b", "qkv.w", "qkv.b", "proj.w", "proj.b", "ls1", "ln2.g", "ln2.b",
+                          "fc1.w", "fc1.b", "fc2.w", "fc2.b", "ls2"})
+      need.push_back("b" + std::to_string(i) + "." + s);
+  for (int i = 0; i < 4; ++i) {
+    need.push_back("proj" + std::to_string(i) + ".w");
+    need.push_back("proj" + std::to_string(i) + ".b");
+    need.push_back("rn" + std::to_string(i + 1) + ".w");
+  }
+  for (int r = 1; r <= 4; ++r) {
+    std::string p = "rf" + std::to_string(r) + ".";
+    need.push_back(p + "out.w");
+    need.push_back(p + "out.b");
+    for (int u = 1; u <= 2; ++u)
+      for (int cc = 1; cc <= 2; ++cc) {
+        need.push_back(p + "rcu" + std::to_string(u) + ".c" + std::to_string(cc) + ".w");
+        need.push_back(p + "rcu" + std::to_string(u) + ".c" + std::to_string(cc) + ".b");
+      }
+  }
+  for (auto& s : need)
+    if (!e->get(s)) {
+      hipFree(e->wmem);
+      std::string m = "packed engine lacks tensor '" + s + "'";
+      delete e;
+      return fail(MDE_ERR_FORMAT, m);
+    }
+  *out = e;
+  return MDE_OK;
+}
+
+// ---- activation arena -----------------------------------------------------
+size_t plan_arena(const mde_engine& e, int B, Buf* b, uint8_t* base) {
+  size_t off = 0;
+  auto take = [&](size_t bytes) -> void* {
+    void* p = base ? (void*)(base + off) : nullptr;
+    off += align_up(bytes, 256);
+    return p;
+  };
+  const size_t bb = (size_t)B;
+  const int D = e.D, F = e.F, np = e.np;
+  const int* oc = e.cfg.out_channels;
+  const size_t s1 = (size_t)(4 * e.ph) * (4 * e.pw), s2 = (size_t)(2 * e.ph) * (2 * e.pw), s3 = np,
+               s4 = (size_t)e.h4 * e.w4;
+  const size_t s0 = (size_t)(8 * e.ph) * (8 * e.pw);
+  Buf t{};
+  t.P = (h16*)take(bb * np * 672 * 2);
+  t.X = (float*)take(bb * e.T * D * 4);
+  t.Hn = (h16*)take(bb * e.T * D * 2);
+  t.Q = (h16*)take(bb * e.H * e.Tpad * 64 * 2);
+  t.K = (h16*)take(bb * e.H * e.Tpad * 64 * 2);
+  t.Vt = (h16*)take(bb * e.H * e.Tpad * 64 * 2);
+  t.O = (h16*)take(bb * e.T * D * 2);
+  t.Mh = (h16*)take(bb * e.T * e.cfg.mlp_hidden * 2);
+  for (int i = 0; i < 4; ++i) t.tap[i] = (h16*)take(bb * np * D * 2);
+  for (int i = 0; i < 4; ++i) t.pj[i] = (h16*)take(bb * np * oc[i] * 2);
+  t.l1 = (h16*)take(bb * s1 * oc[0] * 2);
+  t.l2 = (h16*)take(bb * s2 * oc[1] * 2);
+  t.l4 = (h16*)take(bb * s4 * oc[3] * 2);
+  const size_t ss[4] = {s1, s2, s3, s4};
+  for (int i = 0; i < 4; ++i) t.rn[i] = (h16*)take(bb * ss[i] * F * 2);
+  t.tb = (h16*)take(bb * s1 * F * 2);
+  t.sb = (h16*)take(bb * s1 * F * 2);
+  t.ub = (h16*)take(bb * s1 * F * 2);
+  t.vb = (h16*)take(bb * s1 * F * 2);
+  t.p4 = (h16*)take(bb * s3 * F * 2);
+  t.p3 = (h16*)take(bb * s2 * F * 2);
+  t.p2 = (h16*)take(bb * s1 * F * 2);
+  t.c1 = (h16*)take(bb * s0 * (F / 2) * 2);
+  if (b) *b = t;
+  return off;
+}
+
+// ---- the forward schedule ----------------------------------------------------
+struct Runner {
+  mde_context& c;
+  hipStream_t st;
+  bool prof;
+  hipError_t err = hipSuccess;
+
+  template <class Fn>
+  void step(const char* name, Fn&& fn) {
+    if (err != hipSuccess) return;
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (prof) {
+      if (c.prof_used >= c.prof_events.size()) {
+        hipEvent_t a, b;
+        if ((err = hipEventCreate(&a)) != hipSuccess) return;
+        if ((err = hipEventCreate(&b)) != hipSuccess) return;
+        c.prof_events.push_back({std::string(), {a, b}});
+      }
+      auto& slot = c.prof_events[c.prof_used++];
+      slot.first = name;
+      e0 = slot.second.first;
+      e1 = slot.second.second;
+      if ((err = hipEventRecord(e0, st)) != hipSuccess) return;
+    }
+    err = fn();
+    if (err == hipSuccess && prof) err = hipEventRecord(e1, st);
+  }
+
+  const DevTensor& W(const std::string& n) { return *c.e->get(n); }
+  const h16* w16(const std::string& n) { return (const h16*)W(n).ptr; }
+  const float* w32(const std::string& n) { return (const float*)W(n).ptr; }
+  int ldw(const std::string& n) { return W(n).dims[W(n).ndim - 1]; }
+
+  GemmParams dense(const h16* A, int lda, const std::string& w, int M, int N, int K) {
+    GemmParams g;
+    g.amode = A_DENSE;
+    g.A = A;
+    g.lda = lda;
+    g.W = w16(w);
+    g.ldw = ldw(w);
+    g.M = M;
+    g.N = N;
+    g.K = K;
+    return g;
+  }
+
+  // 3x3 pad-1 conv over NHWC map [B][h][w][cin] -> [B][ho][wo][cout]
+  GemmParams conv(const h16* in, int B, int h, int w, int cin, const std::string& wn, int cout, int stride) {
+    GemmParams g;
+    g.amode = A_CONV3;
+    g.A = in;
+    g.cb = B;
+    g.ch = h;
+    g.cw = w;
+    g.cc = cin;
+    g.stride = stride;
+    g.oh = (h - 1) / stride + 1;
+    g.ow = (w - 1) / stride + 1;
+    g.W = w16(wn);
+    g.ldw = ldw(wn);
+    g.M = B * g.oh * g.ow;
+    g.N = cout;
+    g.K = 9 * cin;
+    g.out16 = nullptr;
+    g.ldo = cout;
+    return g;
+  }
+
+  void gemm(const char* name, const GemmParams& g) {
+    step(name, [&] { return launch_gemm(g, st); });
+  }
+
+  // RCU (pre-activation residual conv unit) at one scale:
+  // out = conv2(relu(conv1(relu(x)) + b1)) + b2 + x (+ extra)
+  void rcu(const std::string& pfx, const h16* x, const h16* extra, h16* out, int B, int h, int w) {
+    const int F = c.e->F;
+    GemmParams g1 = conv(x, B, h, w, F, pfx + ".c1.w", F, 1);
+    g1.relu_in = 1;
+    g1.bias = w32(pfx + ".c1.b");
+    g1.act = ACT_RELU;
+    g1.out16 = c.b.tb;
+    gemm((pfx + ".c1").c_str(), g1);
+    GemmParams g2 = conv(c.b.tb, B, h, w, F, pfx + ".c2.w", F, 1);
+    g2.bias = w32(pfx + ".c2.b");
+    g2.res0 = x;
+    g2.res1 = extra;
+    g2.out16 = out;
+    gemm((pfx + ".c2").c_str(), g2);
+  }
+
+  // FeatureFusionBlock: [x0 + RCU1(x1)] -> RCU2 -> out_conv(1x1) -> resize.
+  // The 1x1 out_conv is applied BEFORE the bilinear resize (both are linear
+  // and bilinear weights sum to 1, so they commute exactly in real
+  // arithmetic); this runs the 1x1 GEMM on 4x fewer pixels.
+  void fusion(int r, const h16* x0, const h16* x1, int B, int h, int w, h16* dst, int oh, int ow) {
+    const std::string p = "rf" + std::to_string(r);
+    const int F = c.e->F;
+    const h16* s = x0;
+    if (x1) {
+      rcu(p + ".rcu1", x1, x0, c.b.sb, B, h, w);
+      s = c.b.sb;
+    }
+    rcu(p + ".rcu2", s, nullptr, c.b.ub, B, h, w);
+    GemmParams g = dense(c.b.ub, F, p + ".out.w", B * h * w, F, F);
+    g.emode = E_STORE;
+    g.bias = w32(p + ".out.b");
+    g.out16 = c.b.vb;
+    g.ldo = F;
+    gemm((p + ".out").c_str(), g);
+    if (dst) step((p + ".resize").c_str(), [&] { return launch_resize(c.b.vb, dst, B, h, w, F, oh, ow, st); });
+  }
+
+  hipError_t forward(int B, const float* img, float* out) {
+    mde_engine& e = *c.e;
+    const PackConfig& cf = e.cfg;
+    const int D = e.D, T = e.T, np = e.np, F = e.F;
+    const int* oc = cf.out_channels;
+    Buf& b = c.b;
+
+    step("patch_prep", [&] {
+      return launch_patch_prep(img, b.P, b.X, w32("pos.cls"), B, cf.img_h, cf.img_w, e.ph, e.pw, T, D, st);
+    });
+    {
+      GemmParams g = dense(b.P, 672, "patch.w", B * np, D, 672);
+      g.emode = E_PATCH;
+      g.bias = w32("patch.b");
+      g.x32 = b.X;
+      g.ldo = D;
+      g.T = T;
+      g.pos = w32("pos.patch");
+      g.npatch = np;
+      gemm("patch_embed", g);
+    }
+    int tap = 0;
+    char nm[64];
+    for (int i = 0; i < cf.depth; ++i) {
+      const std::string p = "b" + std::to_string(i) + ".";
+      snprintf(nm, sizeof nm, "block%d.norm1", i);
+      step(nm, [&] {
+        return launch_layernorm(b.X, b.Hn, w32(p + "ln1.g"), w32(p + "ln1.b"), B * T, D, cf.ln_eps, T, 0, st);
+      });
+      {
+        GemmParams g = dense(b.Hn, D, p + "qkv.w", B * T, 3 * D, D);
+        g.emode = E_QKV;
+        g.bias = w32(p + "qkv.b");
+        g.q = b.Q;
+        g.k = b.K;
+        g.vt = b.Vt;
+        g.T = T;
+        g.Tpad = e.Tpad;
+        g.heads = e.H;
+        g.qscale = 0.125f;  // dh^-0.5, dh = 64 (exact in f16)
+        snprintf(nm, sizeof nm, "block%d.qkv", i);
+        gemm(nm, g);
+      }
+      snprintf(nm, sizeof nm, "block%d.attn", i);
+      step(nm, [&] { return launch_attention(b.Q, b.K, b.Vt, b.O, B, e.H, T, e.Tpad, D, st); });
+      {
+        GemmParams g = dense(b.O, D, p + "proj.w", B * T, D, D);
+        g.emode = E_RESID;
+        g.bias = w32(p + "proj.b");
+        g.ls = w32(p + "ls1");
+        g.x32 = b.X;
+        g.ldo = D;
+        snprintf(nm, sizeof nm, "block%d.proj", i);
+        gemm(nm, g);
+      }
+      snprintf(nm, sizeof nm, "block%d.norm2", i);
+      step(nm, [&] {
+        return launch_layernorm(b.X, b.Hn, w32(p + "ln2.g"), w32(p + "ln2.b"), B * T, D, cf.ln_eps, T, 0, st);
+      });
+      {
+        GemmParams g = dense(b.Hn, D, p + "fc1.w", B * T, cf.mlp_hidden, D);
+        g.emode = E_STORE;
+        g.bias = w32(p + "fc1.b");
+        g.act = ACT_GELU;
+        g.out16 = b.Mh;
+        g.ldo = cf.mlp_hidden;
+        snprintf(nm, sizeof nm, "block%d.fc1", i);
+        gemm(nm, g);
+      }
+      {
+        GemmParams g = dense(b.Mh, cf.mlp_hidden, p + "fc2.w", B * T, D, cf.mlp_hidden);
+        g.emode = E_RESID;
+        g.bias = w32(p + "fc2.b");
+        g.ls = w32(p + "ls2");
+        g.x32 = b.X;
+        g.ldo = D;
+        snprintf(nm, sizeof nm, "block%d.fc2", i);
+        gemm(nm, g);
+      }
+      if (tap < 4 && cf.taps[tap] == i) {
+        snprintf(nm, sizeof nm, "tap%d.norm", tap);
+        h16* dst = b.tap[tap];
+        step(nm, [&] {
+          return launch_layernorm(b.X, dst, w32("norm.g"), w32("norm.b"), B * T, D, cf.ln_eps, T, 1, st);
+        });
+        ++tap;
+      }
+    }
+    if (tap != 4) return hipErrorInvalidValue;
+
+    // ---- DPT head: reassemble ----
+    for (int i = 0; i < 4; ++i) {
+      GemmParams g = dense(b.tap[i], D, "proj" + std::to_string(i) + ".w", B * np, oc[i], D);
+      g.emode = E_STORE;
+      g.bias = w32("proj" + std::to_string(i) + ".b");
+      g.out16 = b.pj[i];
+      g.ldo = oc[i];
+      snprintf(nm, sizeof nm, "reassemble%d.project", i);
+      gemm(nm, g);
+    }
+    {
+      GemmParams g = dense(b.pj[0], oc[0], "rs0.w", B * np, 16 * oc[0], oc[0]);
+      g.emode = E_CONVT;
+      g.bias = w32("rs0.b");
+      g.out16 = b.l1;
+      g.s = 4;
+      g.cout = oc[0];
+      g.ih = e.ph;
+      g.iw = e.pw;
+      gemm("reassemble0.convT4", g);
+    }
+    {
+      GemmParams g = dense(b.pj[1], oc[1], "rs1.w", B * np, 4 * oc[1], oc[1]);
+      g.emode = E_CONVT;
+      g.bias = w32("rs1.b");
+      g.out16 = b.l2;
+      g.s = 2;
+      g.cout = oc[1];
+      g.ih = e.ph;
+      g.iw = e.pw;
+      gemm("reassemble1.convT2", g);
+    }
+    {
+      GemmParams g = conv(b.pj[3], B, e.ph, e.pw, oc[3], "rs3.w", oc[3], 2);
+      g.bias = w32("rs3.b");
+      g.out16 = b.l4;
+      gemm("reassemble3.conv_s2", g);
+    }
+    const int hs[4] = {4 * e.ph, 2 * e.ph, e.ph, e.h4};
+    const int ws[4] = {4 * e.pw, 2 * e.pw, e.pw, e.w4};
+    const h16* lay[4] = {b.l1, b.l2, b.pj[2], b.l4};
+    for (int i = 0; i < 4; ++i) {
+      GemmParams g = conv(lay[i], B, hs[i], ws[i], oc[i], "rn" + std::to_string(i + 1) + ".w", F, 1);
+      g.out16 = b.rn[i];
+      snprintf(nm, sizeof nm, "layer%d_rn", i + 1);
+      gemm(nm, g);
+    }
+    // ---- fusion (refinenet4 .. refinenet1) ----
+    fusion(4, b.rn[3], nullptr, B, hs[3], ws[3], b.p4, hs[2], ws[2]);
+    fusion(3, b.p4, b.rn[2], B, hs[2], ws[2], b.p3, hs[1], ws[1]);
+    fusion(2, b.p3, b.rn[1], B, hs[1], ws[1], b.p2, hs[0], ws[0]);
+    fusion(1, b.p2, b.rn[0], B, hs[0], ws[0], nullptr, 0, 0);  // 1x1 result in vb at hs[0] x ws[0]
+    // ---- head ----
+    const int H1 = 2 * hs[0], W1 = 2 * ws[0];  // refinenet1 upsample x2 (fused into output_conv1's loader)
+    {
+      GemmParams g;
+      g.amode = A_CONV3_UP;
+      g.emode = E_STORE;
+      g.A = b.vb;
+      g.cb = B;
+      g.ch = hs[0];
+      g.cw = ws[0];
+      g.cc = F;
+      g.uh = H1;
+      g.uw = W1;
+      g.oh = H1;
+      g.ow = W1;
+      g.stride = 1;
+      g.W = w16("head.c1.w");
+      g.ldw = ldw("head.c1.w");
+      g.M = B * H1 * W1;
+      g.N = F / 2;
+      g.K = 9 * F;
+      g.bias = w32("head.c1.b");
+      g.out16 = b.c1;
+      g.ldo = F / 2;
+      gemm("head.output_conv1", g);
+    }
+    {
+      const int OH = cf.img_h, OW = cf.img_w;  // (ph*14, pw*14)
+      GemmParams g;
+      g.amode = A_CONV3_UP;
+      g.emode = E_HEAD;
+      g.A = b.c1;
+      g.cb = B;
+      g.ch = H1;
+      g.cw = W1;
+      g.cc = F / 2;
+      g.uh = OH;
+      g.uw = OW;
+      g.oh = OH;
+      g.ow = OW;
+      g.stride = 1;
+      g.W = w16("head.c2.w");
+      g.ldw = ldw("head.c2.w");
+      g.M = B * OH * OW;
+      g.N = cf.head_hidden;
+      g.K = 9 * (F / 2);
+      g.bias = w32("head.c2.b");
+      g.w2 = w32("head.c3.w");
+      g.b2 = e.head_b2;
+      g.head_metric = cf.metric;
+      g.max_depth = cf.max_depth;
+      g.out32 = out;
+      gemm("head.output_conv2", g);
+    }
+    return err;
+  }
+};
+
+int check_ctx(const mde_context* c) {
+  if (!c || !c->e) return fail(MDE_ERR_ARG, "null context");
+  return MDE_OK;
+}
+
+bool is_input(const char* n) { return n && strcmp(n, "input") == 0; }
+bool is_output(const char* n) { return n && strcmp(n, "output") == 0; }
+
+}  // namespace
+
+// ============================== C ABI ======================================
+extern "C" {
+
+int mde_version(void) { return MDE_ABI_VERSION; }
+const char* mde_last_error(void) { return g_err.c_str(); }
+
+int mde_engine_load_memory(const void* data, size_t nbytes, int device, mde_engine** out) {
+  if (!data || !out) return fail(MDE_ERR_ARG, "null argument");
+  *out = nullptr;
+  int rc = load_pack((const uint8_t*)data, nbytes, device, out);
+  if (rc != MDE_OK) return rc;
+  // the head's 1x1 bias scalar, stashed host-side for the kernel argument
+  mde_engine* e = *out;
+  hipError_t he = hipMemcpy(&e->head_b2, e->get("head.c3.b")->ptr, 4, hipMemcpyDeviceToHost);
+  if (he != hipSuccess) {
+    mde_engine_destroy(e);
+    *out = nullptr;
+    return hip_fail(he, "reading head bias");
+  }
+  return MDE_OK;
+}
+
+int mde_engine_load(const char* path, int device, mde_engine** out) {
+  if (!path || !out) return fail(MDE_ERR_ARG, "null argument");
+  FILE* f = fopen(path, "rb");
+  if (!f) return fail(MDE_ERR_FILE, std::string("cannot open packed engine ") + path);
+  std::vector<uint8_t> buf;
+  fseek(f, 0, SEEK_END);
+  long n = ftell(f);
+  fseek(f, 0, SEEK_SET);
+  if (n <= 0) {
+    fclose(f);
+    return fail(MDE_ERR_FILE, std::string("empty packed engine ") + path);
+  }
+  buf.resize((size_t)n);
+  size_t got = fread(buf.data(), 1, (size_t)n, f);
+  fclose(f);
+  if (got != (size_t)n) return fail(MDE_ERR_FILE, std::string("short read of ") + path);
+  return mde_engine_load_memory(buf.data(), buf.size(), device, out);
+}
+
+int mde_engine_destroy(mde_engine* e) {
+  if (!e) return MDE_OK;
+  hipSetDevice(e->device);
+  if (e->wmem) hipFree(e->wmem);
+  delete e;
+  return MDE_OK;
+}
+
+int mde_engine_get_info(const mde_engine* e, mde_engine_info* o) {
+  if (!e || !o) return fail(MDE_ERR_ARG, "null argument");
+  memset(o, 0, sizeof *o);
+  const PackConfig& c = e->cfg;
+  memcpy(o->encoder, c.encoder, sizeof o->encoder);
+  o->encoder[sizeof o->encoder - 1] = 0;
+  o->embed_dim = c.embed_dim;
+  o->depth = c.depth;
+  o->num_heads = c.num_heads;
+  o->mlp_hidden = c.mlp_hidden;
+  o->patch = c.patch;
+  o->img_h = c.img_h;
+  o->img_w = c.img_w;
+  o->features = c.features;
+  o->head_hidden = c.head_hidden;
+  o->metric = c.metric;
+  for (int i = 0; i < 4; ++i) {
+    o->out_channels[i] = c.out_channels[i];
+    o->taps[i] = c.taps[i];
+  }
+  o->max_depth = c.max_depth;
+  o->ln_eps = c.ln_eps;
+  o->max_batch_hint = 64;
+  o->weight_bytes = (int64_t)e->wbytes;
+  return MDE_OK;
+}
+
+int mde_engine_num_io(const mde_engine* e, int* n) {
+  if (!e || !n) return fail(MDE_ERR_ARG, "null argument");
+  *n = 2;
+  return MDE_OK;
+}
+
+int mde_engine_io_desc(const mde_engine* e, int index, mde_io_desc* o) {
+  if (!e || !o) return fail(MDE_ERR_ARG, "null argument");
+  memset(o, 0, sizeof *o);
+  if (index == 0) {
+    strcpy(o->name, "input");
+    o->dtype = MDE_FLOAT32;
+    o->is_input = 1;
+    o->rank = 4;
+    o->dims[0] = -1;
+    o->dims[1] = 3;
+    o->dims[2] = e->cfg.img_h;
+    o->dims[3] = e->cfg.img_w;
+  } else if (index == 1) {
+    strcpy(o->name, "output");
+    o->dtype = MDE_FLOAT32;
+    o->is_input = 0;
+    o->rank = 3;
+    o->dims[0] = -1;
+    o->dims[1] = e->cfg.img_h;
+    o->dims[2] = e->cfg.img_w;
+  } else {
+    return fail(MDE_ERR_ARG, "io index out of range");
+  }
+  return MDE_OK;
+}
+
+int mde_engine_profile_shape(const mde_engine* e, const char* name, int which, int64_t* dims, int* rank) {
+  if (!e || !name || !dims || !rank) return fail(MDE_ERR_ARG, "null argument");
+  if (which < 0 || which > 2) return fail(MDE_ERR_ARG, "which must be 0 (min), 1 (opt) or 2 (max)");
+  const int64_t bsel[3] = {1, 1, 64};
+  mde_io_desc d;
+  int idx = is_input(name) ? 0 : is_output(name) ? 1 : -1;
+  if (idx < 0) return fail(MDE_ERR_NAME, std::string("unknown tensor ") + name);
+  mde_engine_io_desc(e, idx, &d);
+  *rank = d.rank;
+  for (int i = 0; i < d.rank; ++i) dims[i] = d.dims[i];
+  dims[0] = bsel[which];
+  return MDE_OK;
+}
+
+int mde_context_create(mde_engine* e, int max_batch, mde_context** out) {
+  if (!e || !out || max_batch < 1) return fail(MDE_ERR_ARG, "bad argument to mde_context_create");
+  *out = nullptr;
+  HIP_OR(hipSetDevice(e->device), "hipSetDevice");
+  auto* c = new mde_context();
+  c->e = e;
+  c->device = e->device;
+  c->max_batch = max_batch;
+  c->batch = 1;
+  c->arena_bytes = plan_arena(*e, max_batch, nullptr, nullptr);
+  hipError_t he = hipMalloc(&c->arena, c->arena_bytes);
+  if (he != hipSuccess) {
+    delete c;
+    return hip_fail(he, "hipMalloc(activation arena)");
+  }
+  plan_arena(*e, max_batch, &c->b, (uint8_t*)c->arena);
+  // zero once: the q/k/v^T pad rows/columns beyond T must stay 0
+  he = hipMemset(c->arena, 0, c->arena_bytes);
+  if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking);
+  if (he == hipSuccess) he = hipDeviceSynchronize();
+  if (he != hipSuccess) {
+    hipFree(c->arena);
+    delete c;
+    return hip_fail(he, "context init");
+  }
+  *out = c;
+  return MDE_OK;
+}
+
+int mde_context_destroy(mde_context* c) {
+  if (!c) return MDE_OK;
+  hipSetDevice(c->device);
+  for (auto& kv : c->graphs) {
+    hipGraphExecDestroy(kv.second.second);
+    hipGraphDestroy(kv.second.first);
+  }
+  for (auto& pe : c->prof_events) {
+    hipEventDestroy(pe.second.first);
+    hipEventDestroy(pe.second.second);
+  }
+  if (c->cap_stream) hipStreamDestroy(c->cap_stream);
+  if (c->arena) hipFree(c->arena);
+  delete c;
+  return MDE_OK;
+}
+
+int mde_context_set_tensor_address(mde_context* c, const char* name, void* ptr) {
+  if (int rc = check_ctx(c)) return rc;
+  if (is_input(name)) c->in = ptr;
+  else if (is_output(name)) c->out = ptr;
+  else return fail(MDE_ERR_NAME, std::string("unknown tensor ") + (name ? name : "(null)"));
+  return MDE_OK;
+}
+
+int mde_context_set_input_shape(mde_context* c, const char* name, const int64_t* dims, int rank) {
+  if (int rc = check_ctx(c)) return rc;
+  if (!is_input(name)) return fail(MDE_ERR_NAME, std::string("not an input: ") + (name ? name : "(null)"));
+  if (!dims || rank != 4) return fail(MDE_ERR_SHAPE, "input shape must be rank 4 [B,3,H,W]");
+  const PackConfig& cf = c->e->cfg;
+  if (dims[1] != 3 || dims[2] != cf.img_h || dims[3] != cf.img_w)
+    return fail(MDE_ERR_SHAPE, "input shape must be [B,3," + std::to_string(cf.img_h) + "," +
+                                   std::to_string(cf.img_w) + "] for this engine");
+  if (dims[0] < 1 || dims[0] > c->max_batch)
+    return fail(MDE_ERR_SHAPE, "batch " + std::to_string(dims[0]) + " outside [1, " +
+                                   std::to_string(c->max_batch) + "]");
+  c->batch = (int)dims[0];
+  return MDE_OK;
+}
+
+int mde_context_get_tensor_shape(const mde_context* c, const char* name, int64_t* dims, int* rank) {
+  if (int rc = check_ctx(c)) return rc;
+  if (!dims || !rank) return fail(MDE_ERR_ARG, "null argument");
+  mde_io_desc d;
+  int idx = is_input(name) ? 0 : is_output(name) ? 1 : -1;
+  if (idx < 0) return fail(MDE_ERR_NAME, std::string("unknown tensor ") + (name ? name : "(null)"));
+  mde_engine_io_desc(c->e, idx, &d);
+  *rank = d.rank;
+  for (int i = 0; i < d.rank; ++i) dims[i] = d.dims[i];
+  dims[0] = c->batch;
+  return MDE_OK;
+}
+
+int mde_context_set_graph_mode(mde_context* c, int enable) {
+  if (int rc = check_ctx(c)) return rc;
+  c->graph_mode = enable != 0;
+  return MDE_OK;
+}
+
+int mde_context_set_profiler(mde_context* c, mde_layer_cb cb, void* user) {
+  if (int rc = check_ctx(c)) return rc;
+  c->prof_cb = cb;
+  c->prof_user = user;
+  return MDE_OK;
+}
+
+int mde_context_workspace_bytes(const mde_context* c, size_t* bytes) {
+  if (int rc = check_ctx(c)) return rc;
+  if (!bytes) return fail(MDE_ERR_ARG, "null argument");
+  *bytes = c->arena_bytes;
+  return MDE_OK;
+}
+
+int mde_context_enqueue(mde_context* c, void* stream) {
+  if (int rc = check_ctx(c)) return rc;
+  if (!c->in || !c->out) return fail(MDE_ERR_STATE, "set_tensor_address('input'/'output') before enqueue");
+  hipStream_t st = (hipStream_t)stream;
+  HIP_OR(hipSetDevice(c->e->device), "hipSetDevice");
+  const float* in = (const float*)c->in;
+  float* out = (float*)c->out;
+  if (c->prof_cb) {
+    c->prof_used = 0;
+    Runner r{*c, st, true};
+    hipError_t he = r.forward(c->batch, in, out);
+    if (he != hipSuccess) return hip_fail(he, "enqueue (profiled)");
+    HIP_OR(hipStreamSynchronize(st), "hipStreamSynchronize");
+    for (size_t i = 0; i < c->prof_used; ++i) {
+      float ms = 0.f;
+      hipEventElapsedTime(&ms, c->prof_events[i].second.first, c->prof_events[i].second.second);
+      c->prof_cb(c->prof_events[i].first.c_str(), ms, c->prof_user);
+    }
+    return MDE_OK;
+  }
+  if (!c->graph_mode) {
+    Runner r{*c, st, false};
+    hipError_t he = r.forward(c->batch, in, out);
+    if (he != hipSuccess) return hip_fail(he, "enqueue");
+    return MDE_OK;
+  }
+  GraphKey key{c->batch, c->in, c->out};
+  auto it = c->graphs.find(key);
+  if (it == c->graphs.end()) {
+    hipGraph_t g = nullptr;
+    hipGraphExec_t ge = nullptr;
+    HIP_OR(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
+    Runner r{*c, c->cap_stream, false};
+    hipError_t he = r.forward(c->batch, in, out);
+    hipError_t he2 = hipStreamEndCapture(c->cap_stream, &g);
+    if (he != hipSuccess) {
+      if (g) hipGraphDestroy(g);
+      return hip_fail(he, "capture forward");
+    }
+    if (he2 != hipSuccess) return hip_fail(he2, "hipStreamEndCapture");
+    he = hipGraphInstantiate(&ge, g, nullptr, nullptr, 0);
+    if (he != hipSuccess) {
+      hipGraphDestroy(g);
+      return hip_fail(he, "hipGraphInstantiate");
+    }
+    it = c->graphs.emplace(key, std::make_pair(g, ge)).first;
+  }
+  HIP_OR(hipGraphLaunch(it->second.second, st), "hipGraphLaunch");
+  return MDE_OK;
+}
+
+// ---- runtime helpers --------------------------------------------------------
+int mde_rt_device_count(int* n) {
+  if (!n) return fail(MDE_ERR_ARG, "null argument");
+  HIP_OR(hipGetDeviceCount(n), "hipGetDeviceCount");
+  return MDE_OK;
+}
+int mde_rt_set_device(int d) {
+  HIP_OR(hipSetDevice(d), "hipSetDevice");
+  return MDE_OK;
+}
+int mde_rt_device_name(int d, char* buf, int len) {
+  if (!buf || len <= 0) return fail(MDE_ERR_ARG, "null argument");
+  hipDeviceProp_t p;
+  HIP_OR(hipGetDeviceProperties(&p, d), "hipGetDeviceProperties");
+  snprintf(buf, (size_t)len, "%s (%s)", p.name, p.gcnArchName);
+  return MDE_OK;
+}
+int mde_rt_malloc(void** p, size_t n) {
+  if (!p) return fail(MDE_ERR_ARG, "null argument");
+  HIP_OR(hipMalloc(p, n), "hipMalloc");
+  return MDE_OK;
+}
+int mde_rt_free(void* p) {
+  HIP_OR(hipFree(p), "hipFree");
+  return MDE_OK;
+}
+int mde_rt_malloc_host(void** p, size_t n) {
+  if (!p) return fail(MDE_ERR_ARG, "null argument");
+  HIP_OR(hipHostMalloc(p, n, hipHostMallocDefault), "hipHostMalloc");
+  return MDE_OK;
+}
+int mde_rt_free_host(void* p) {
+  HIP_OR(hipHostFree(p), "hipHostFree");
+  return MDE_OK;
+}
+int mde_rt_memcpy_htod_async(void* d, const void* s, size_t n, void* st) {
+  HIP_OR(hipMemcpyAsync(d, s, n, hipMemcpyHostToDevice, (hipStream_t)st), "hipMemcpyAsync(H2D)");
+  return MDE_OK;
+}
+int mde_rt_memcpy_dtoh_async(void* d, const void* s, size_t n, void* st) {
+  HIP_OR(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToHost, (hipStream_t)st), "hipMemcpyAsync(D2H)");
+  return MDE_OK;
+}
+int mde_rt_memcpy_dtod_async(void* d, const void* s, size_t n, void* st) {
+  HIP_OR(hipMemcpyAsync(d, s, n, hipMemcpyDeviceToDevice, (hipStream_t)st), "hipMemcpyAsync(D2D)");
+  return MDE_OK;
+}
+int mde_rt_memset_async(void* d, int v, size_t n, void* st) {
+  HIP_OR(hipMemsetAsync(d, v, n, (hipStream_t)st), "hipMemsetAsync");
+  return MDE_OK;
+}
+int mde_rt_stream_create(void** s) {
+  if (!s) return fail(MDE_ERR_ARG, "null argument");
+  hipStream_t st;
+  HIP_OR(hipStreamCreateWithFlags(&st, hipStreamNonBlocking), "hipStreamCreate");
+  *s = st;
+  return MDE_OK;
+}
+int mde_rt_stream_destroy(void* s) {
+  HIP_OR(hipStreamDestroy((hipStream_t)s), "hipStreamDestroy");
+  return MDE_OK;
+}
+int mde_rt_stream_synchronize(void* s) {
+  HIP_OR(hipStreamSynchronize((hipStream_t)s), "hipStreamSynchronize");
+  return MDE_OK;
+}
+int mde_rt_device_synchronize(void) {
+  HIP_OR(hipDeviceSynchronize(), "hipDeviceSynchronize");
+  return MDE_OK;
+}
+int mde_rt_event_create(void** e) {
+  if (!e) return fail(MDE_ERR_ARG, "null argument");
+  hipEvent_t ev;
+  HIP_OR(hipEventCreate(&ev), "hipEventCreate");
+  *e = ev;
+  return MDE_OK;
+}
+int mde_rt_event_destroy(void* e) {
+  HIP_OR(hipEventDestroy((hipEvent_t)e), "hipEventDestroy");
+  return MDE_OK;
+}
+int mde_rt_event_record(void* e, void* s) {
+  HIP_OR(hipEventRecord((hipEvent_t)e, (hipStream_t)s), "hipEventRecord");
+  return MDE_OK;
+}
+int mde_rt_event_elapsed_ms(float* ms, void* a, void* b) {
+  if (!ms) return fail(MDE_ERR_ARG, "null argument");
+  HIP_OR(hipEventElapsedTime(ms, (hipEvent_t)a, (hipEvent_t)b), "hipEventElapsedTime");
+  return MDE_OK;
+}
+
+// ---- kernel-level entry points ------------------------------------------------
+#define OP_RET(call, what)                                   \
+  do {                                                       \
+    hipError_t e_ = (call);                                  \
+    if (e_ == hipErrorInvalidValue) return fail(MDE_ERR_ARG, what ": invalid shape/argument"); \
+    if (e_ != hipSuccess) return hip_fail(e_, what);          \
+    return MDE_OK;                                           \
+  } while (0)
+
+int mde_op_layernorm(const float* x, void* y, const float* g, const float* b, int rows, int dim, float eps,
+                     int tokens, int skip_cls, void* st) {
+  if (!x || !y || !g || !b) return fail(MDE_ERR_ARG, "null argument");
+  if (skip_cls && tokens < 2) return fail(MDE_ERR_ARG, "skip_cls needs tokens >= 2");
+  OP_RET(launch_layernorm(x, (h16*)y, g, b, rows, dim, eps, tokens > 0 ? tokens : 1, skip_cls, (hipStream_t)st),
+         "layernorm");
+}
+
+int mde_op_linear(const void* a, int lda, const void* w, int ldw, int m, int n, int k, const float* bias, int act,
+                  void* out, int ldo, void* st) {
+  if (!a || !w || !out) return fail(MDE_ERR_ARG, "null argument");
+  GemmParams g;
+  g.A = (const h16*)a;
+  g.lda = lda;
+  g.W = (const h16*)w;
+  g.ldw = ldw;
+  g.M = m;
+  g.N = n;
+  g.K = k;
+  g.bias = bias;
+  g.act = act;
+  g.out16 = (h16*)out;
+  g.ldo = ldo;
+  OP_RET(launch_gemm(g, (hipStream_t)st), "linear");
+}
+
+int mde_op_linear_residual(const void* a, int lda, const void* w, int ldw, int m, int n, int k, const float* bias,
+                           const float* ls, float* x32, int ldx, void* st) {
+  if (!a || !w || !bias || !ls || !x32) return fail(MDE_ERR_ARG, "null argument");
+  GemmParams g;
+  g.emode = E_RESID;
+  g.A = (const h16*)a;
+  g.lda = lda;
+  g.W = (const h16*)w;
+  g.ldw = ldw;
+  g.M = m;
+  g.N = n;
+  g.K = k;
+  g.bias = bias;
+  g.ls = ls;
+  g.x32 = x32;
+  g.ldo = ldx;
+  OP_RET(launch_gemm(g, (hipStream_t)st), "linear_residual");
+}
+
+int mde_op_qkv(const void* a, const void* w, int ldw, const float* bias, int batch, int tokens, int heads,
+               int tokens_pad, float qscale, void* q, void* k, void* vt, void* st) {
+  if (!a || !w || !bias || !q || !k || !vt) return fail(MDE_ERR_ARG, "null argument");
+  if (tokens_pad < tokens) return fail(MDE_ERR_ARG, "tokens_pad < tokens");
+  GemmParams g;
+  g.emode = E_QKV;
+  const int D = heads * 64;
+  g.A = (const h16*)a;
+  g.lda = D;
+  g.W = (const h16*)w;
+  g.ldw = ldw;
+  g.M = batch * tokens;
+  g.N = 3 * D;
+  g.K = D;
+  g.bias = bias;
+  g.q = (h16*)q;
+  g.k = (h16*)k;
+  g.vt = (h16*)vt;
+  g.T = tokens;
+  g.Tpad = tokens_pad;
+  g.heads = heads;
+  g.qscale = qscale;
+  OP_RET(launch_gemm(g, (hipStream_t)st), "qkv");
+}
+
+int mde_op_attention(const void* q, const void* k, const void* vt, void* o, int batch, int heads, int tokens,
+                     int tokens_pad, int ldo, void* st) {
+  if (!q || !k || !vt || !o) return fail(MDE_ERR_ARG, "null argument");
+  OP_RET(launch_attention((const h16*)q, (const h16*)k, (const h16*)vt, (h16*)o, batch, heads, tokens, tokens_pad,
+                          ldo, (hipStream_t)st),
+         "attention");
+}
+
+int mde_op_patch_embed(const float* img, int batch, int h, int w, const void* wt, int ldw, const float* bias,
+                       const float* pos_patch, const float* cls_pos, int dim, void* scratch, float* x32, void* st) {
+  if (!img || !wt || !bias || !pos_patch || !cls_pos || !scratch || !x32) return fail(MDE_ERR_ARG, "null argument");
+  if (h % 14 || w % 14) return fail(MDE_ERR_ARG, "image size must be a multiple of 14");
+  const int ph = h / 14, pw = w / 14, T = ph * pw + 1;
+  hipError_t e = launch_patch_prep(img, (h16*)scratch, x32, cls_pos, batch, h, w, ph, pw, T, dim, (hipStream_t)st);
+  if (e != hipSuccess) return hip_fail(e, "patch_prep");
+  GemmParams g;
+  g.emode = E_PATCH;
+  g.A = (const h16*)scratch;
+  g.lda = 672;
+  g.W = (const h16*)wt;
+  g.ldw = ldw;
+  g.M = batch * ph * pw;
+  g.N = dim;
+  g.K = 672;
+  g.bias = bias;
+  g.x32 = x32;
+  g.ldo = dim;
+  g.T = T;
+  g.pos = pos_patch;
+  g.npatch = ph * pw;
+  OP_RET(launch_gemm(g, (hipStream_t)st), "patch_embed");
+}
+
+int mde_op_conv3x3(const void* in, int batch, int h, int w, int cin, const void* wt, int ldw, int cout, int stride,
+                   int relu_in, const float* bias, int act, const void* res0, const void* res1, void* out,
+                   void* st) {
+  if (!in || !wt || !out) return fail(MDE_ERR_ARG, "null argument");
+  if (stride != 1 && stride != 2) return fail(MDE_ERR_ARG, "stride must be 1 or 2");
+  GemmParams g;
+  g.amode = A_CONV3;
+  g.A = (const h16*)in;
+  g.cb = batch;
+  g.ch = h;
+  g.cw = w;
+  g.cc = cin;
+  g.stride = stride;
+  g.oh = (h - 1) / stride + 1;
+  g.ow = (w - 1) / stride + 1;
+  g.W = (const h16*)wt;
+  g.ldw = ldw;
+  g.M = batch * g.oh * g.ow;
+  g.N = cout;
+  g.K = 9 * cin;
+  g.relu_in = relu_in;
+  g.bias = bias;
+  g.act = act;
+  g.res0 = (const h16*)res0;
+  g.res1 = (const h16*)res1;
+  g.out16 = (h16*)out;
+  g.ldo = cout;
+  OP_RET(launch_gemm(g, (hipStream_t)st), "conv3x3");
+}
+
+int mde_op_conv3x3_up(const void* in, int batch, int sh, int sw, int cin, int uh, int uw, const void* wt, int ldw,
+                      int cout, const float* bias, int act, void* out, void* st) {
+  if (!in || !wt || !out) return fail(MDE_ERR_ARG, "null argument");
+  GemmParams g;
+  g.amode = A_CONV3_UP;
+  g.A = (const h16*)in;
+  g.cb = batch;
+  g.ch = sh;
+  g.cw = sw;
+  g.cc = cin;
+  g.uh = uh;
+  g.uw = uw;
+  g.oh = uh;
+  g.ow = uw;
+  g.stride = 1;
+  g.W = (const h16*)wt;
+  g.ldw = ldw;
+  g.M = batch * uh * uw;
+  g.N = cout;
+  g.K = 9 * cin;
+  g.bias = bias;
+  g.act = act;
+  g.out16 = (h16*)out;
+  g.ldo = cout;
+  OP_RET(launch_gemm(g, (hipStream_t)st), "conv3x3_up");
+}
+
+int mde_op_conv_transpose(const void* in, int batch, int h, int w, int cin, const void* wt, int ldw, int cout,
+                          int stride, const float* bias, void* out, void* st) {
+  if (!in || !wt || !bias || !out) return fail(MDE_ERR_ARG, "null argument");
+  GemmParams g;
+  g.emode = E_CONVT;
+  g.A = (const h16*)in;
+  g.lda = cin;
+  g.W = (const h16*)wt;
+  g.ldw = ldw;
+  g.M = batch * h * w;
+  g.N = stride * stride * cout;
+  g.K = cin;
+  g.bias = bias;
+  g.out16 = (h16*)out;
+  g.s = stride;
+  g.cout = cout;
+  g.ih = h;
+  g.iw = w;
+  OP_RET(launch_gemm(g, (hipStream_t)st), "conv_transpose");
+}
+
+int mde_op_resize_bilinear(const void* in, int batch, int ih, int iw, int c, int oh, int ow, void* out, void* st) {
+  if (!in || !out) return fail(MDE_ERR_ARG, "null argument");
+  OP_RET(launch_resize((const h16*)in, (h16*)out, batch, ih, iw, c, oh, ow, (hipStream_t)st), "resize_bilinear");
+}
+
+int mde_op_depth_head(const void* in, int batch, int sh, int sw, int cin, int uh, int uw, const void* wt, int ldw,
+                      const float* bias, const float* w2, float b2, int metric, float max_depth, float* out,
+                      void* st) {
+  if (!in || !wt || !bias || !w2 || !out) return fail(MDE_ERR_ARG, "null argument");
+  GemmParams g;
+  g.amode = A_CONV3_UP;
+  g.emode = E_HEAD;
+  g.A = (const h16*)in;
+  g.cb = batch;
+  g.ch = sh;
+  g.cw = sw;
+  g.cc = cin;
+  g.uh = uh;
+  g.uw = uw;
+  g.oh = uh;
+  g.ow = uw;
+  g.stride = 1;
+  g.W = (const h16*)wt;
+  g.ldw = ldw;
+  g.M = batch * uh * uw;
+  g.N = 32;
+  g.K = 9 * cin;
+  g.bias = bias;
+  g.w2 = w2;
+  g.b2 = b2;
+  g.head_metric = metric;
+  g.max_depth = max_depth;
+  g.out32 = out;
+  OP_RET(launch_gemm(g, (hipStream_t)st), "depth_head");
+}
+
+}  // extern "C"

@@ -1,0 +1,70 @@
+// Host-side launch interface of the hot-path kernels (internal to libmde_hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace mde {
+
+typedef _Float16 h16;
+
+// How the A operand (rows = output pixels / tokens, K contiguous) is formed.
+enum AMode : int {
+  A_DENSE = 0,    // A[m*lda + k], row-major f16
+  A_CONV3 = 1,    // implicit im2col of a 3x3 pad-1 conv over an NHWC f16 map
+  A_CONV3_UP = 2  // same, over bilinear(align_corners=True)-upsampled NHWC map
+};
+
+// What the epilogue does with acc[m][n] (fp32).
+enum EMode : int {
+  E_STORE = 0,   // out16[m*ldo+n] = act(acc + bias[n]) (+ res0 + res1)
+  E_QKV = 1,     // scatter to head-major q (pre-scaled), k and transposed v
+  E_RESID = 2,   // x32[m*ldo+n] += ls[n] * (acc + bias[n])
+  E_PATCH = 3,   // x32[(b*T+1+p)*ldo+n] = acc + bias[n] + pos[p*ldo+n]
+  E_CONVT = 4,   // ConvTranspose(k=s) pixel-shuffle store into NHWC f16
+  E_HEAD = 5     // relu(acc+bias) . w2 + b2 -> sigmoid*max | relu -> fp32 map
+};
+
+enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
+
+struct GemmParams {
+  int amode = A_DENSE, emode = E_STORE;
+  int M = 0, N = 0, K = 0;
+  const h16* A = nullptr; int lda = 0;
+  const h16* W = nullptr; int ldw = 0;  // weights [Npad][ldw], ldw % 32 == 0
+  // conv geometry: source NHWC map [cb][ch][cw][cc]; output map [cb][oh][ow]
+  int cb = 0, ch = 0, cw = 0, cc = 0;
+  int uh = 0, uw = 0;  // virtual (upsampled) input size, A_CONV3_UP
+  int oh = 0, ow = 0, stride = 1;
+  int relu_in = 0;
+  // epilogue
+  const float* bias = nullptr; int act = ACT_NONE;
+  h16* out16 = nullptr; int ldo = 0;
+  const h16* res0 = nullptr; const h16* res1 = nullptr;
+  float* x32 = nullptr; const float* ls = nullptr;
+  // E_QKV
+  h16 *q = nullptr, *k = nullptr, *vt = nullptr;
+  int T = 0, Tpad = 0, heads = 0; float qscale = 1.0f;
+  // E_PATCH
+  const float* pos = nullptr; int npatch = 0;
+  // E_CONVT
+  int s = 0, cout = 0, ih = 0, iw = 0;
+  // E_HEAD
+  const float* w2 = nullptr; float b2 = 0.f; int head_metric = 1; float max_depth = 1.f;
+  float* out32 = nullptr;
+};
+
+hipError_t launch_gemm(const GemmParams& p, hipStream_t st);
+
+hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T,
+                            int Tpad, int ldo, hipStream_t st);
+
+hipError_t launch_layernorm(const float* x, h16* y, const float* g, const float* b, int rows, int D,
+                            float eps, int T, int skip_cls, hipStream_t st);
+
+hipError_t launch_patch_prep(const float* img, h16* P, float* X, const float* cls_pos, int B, int H,
+                             int W, int ph, int pw, int T, int D, hipStream_t st);
+
+hipError_t launch_resize(const h16* in, h16* out, int B, int ih, int iw, int C, int oh, int ow,
+                         hipStream_t st);
+
+}  // namespace mde

@@ -1,0 +1,50 @@
+// On-disk layout of a packed DA-V2 engine (written by pack.py, read by
+// engine.hip).  Little-endian, fixed-size records.
+//
+//   [0]            PackHeader   (32 B)
+//   [32]           PackConfig   (256 B)
+//   [288]          PackTensor x n_tensors (128 B each)
+//   [data_offset]  tensor bytes, each at data_offset + PackTensor.offset
+//                  (offsets 256-byte aligned)
+#pragma once
+#include <stdint.h>
+
+namespace mde {
+
+#pragma pack(push, 1)
+struct PackHeader {
+  char magic[8];  // "MDEPACK1"
+  uint32_t version;
+  uint32_t n_tensors;
+  uint64_t data_offset;
+  uint64_t data_bytes;
+};
+static_assert(sizeof(PackHeader) == 32, "PackHeader");
+
+struct PackConfig {
+  int32_t embed_dim, depth, num_heads, mlp_hidden, patch;
+  int32_t img_h, img_w, features;
+  int32_t out_channels[4];
+  int32_t taps[4];
+  int32_t head_hidden, metric;
+  float max_depth, ln_eps;
+  char encoder[16];
+  char reserved[160];
+};
+static_assert(sizeof(PackConfig) == 256, "PackConfig");
+
+struct PackTensor {
+  char name[80];
+  int32_t dtype;  // 0 f32, 1 f16
+  int32_t ndim;
+  int32_t dims[4];
+  uint64_t offset;
+  uint64_t nbytes;
+  char reserved[8];
+};
+static_assert(sizeof(PackTensor) == 128, "PackTensor");
+#pragma pack(pop)
+
+constexpr uint32_t kPackVersion = 1;
+
+}  // namespace mde

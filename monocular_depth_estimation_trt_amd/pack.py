@@ -1,0 +1,222 @@
+"""AOT weight packer: DA-V2 state dict -> packed engine file for libmde_hip.
+
+Replaces the reference's export/build stage -- `run.py export` ->
+`models/depth_anything_v2/onnx_export.py:19-100` (ONNX opset 20 + onnxsim)
+and `run.py build` -> `core/common.py:166-274` (TensorRT builder) -- with one
+deterministic host-side pass that lays the weights out for the gfx950 kernels:
+
+* every matrix operand becomes f16 [Npad][Kpad] (K contiguous; N padded to a
+  multiple of 128 and K to a multiple of 32 with zeros) -- the B-operand
+  layout of the MFMA GEMM (csrc/gemm.hip);
+* 3x3 conv weights [Cout][Cin][3][3] -> [Cout][ky][kx][Cin] (the implicit
+  im2col K order over an NHWC map);
+* ConvTranspose(k == s) weights [Cin][Cout][s][s] -> [(dy*s+dx)*Cout+co][Cin]
+  (a plain GEMM whose epilogue pixel-shuffles);
+* patch-embed [D][3][14][14] -> [D][3*14*16] (kx padded to 16 so every 8-wide
+  K chunk of the im2col row is 16-byte aligned);
+* the positional table is interpolated ONCE for the packed input size with
+  upstream DINOv2's bicubic + 0.1-offset rule, and cls + pos[0] is folded;
+* LayerNorm / LayerScale / bias vectors stay fp32.
+
+File layout: csrc/pack_format.h.  A packed file is specific to one model
+variant and one input size, like a TensorRT engine is to its profile.
+"""
+
+from __future__ import annotations
+
+import hashlib
+import math
+import os
+import struct
+from collections import OrderedDict
+from typing import Dict, Tuple
+
+import numpy as np
+
+from . import weights as W
+
+PACK_VERSION = 1
+PACKER_VERSION = "mde-pack-1"
+ALIGN = 256
+
+
+def _pad2(a: np.ndarray, n_mult: int = 128, k_mult: int = 32) -> np.ndarray:
+    n, k = a.shape
+    N = -(-n // n_mult) * n_mult
+    K = -(-k // k_mult) * k_mult
+    out = np.zeros((N, K), np.float16)
+    out[:n, :k] = a.astype(np.float16)
+    return out
+
+
+def _conv3(w: np.ndarray) -> np.ndarray:
+    """[Cout][Cin][3][3] -> f16 [Cout_pad][9*Cin pad32] in (ky, kx, ci) order."""
+    co, ci, kh, kw = w.shape
+    assert kh == 3 and kw == 3, w.shape
+    return _pad2(np.ascontiguousarray(w.transpose(0, 2, 3, 1)).reshape(co, 9 * ci))
+
+
+def _convT(w: np.ndarray) -> np.ndarray:
+    """ConvTranspose2d weight [Cin][Cout][s][s] (k == s) -> [(dy*s+dx)*Cout+co][Cin]."""
+    ci, co, s, s2 = w.shape
+    assert s == s2
+    return _pad2(np.ascontiguousarray(w.transpose(2, 3, 1, 0)).reshape(s * s * co, ci))
+
+
+def interpolate_pos_embed(pos: np.ndarray, ph: int, pw: int) -> np.ndarray:
+    """Upstream DINOv2 interpolate_pos_encoding (bicubic, scale_factor with the
+    0.1 offset, antialias False).  [1, 1+M*M, D] -> [1, 1+ph*pw, D] fp32."""
+    N = pos.shape[1] - 1
+    if N == ph * pw and ph == pw:
+        return pos.astype(np.float32)
+    import torch
+    import torch.nn.functional as F
+    M = int(math.isqrt(N))
+    if M * M != N:
+        raise ValueError(f"pos_embed has {N} patch positions, not a square grid")
+    D = pos.shape[-1]
+    t = torch.from_numpy(np.ascontiguousarray(pos, dtype=np.float32))
+    patch = t[:, 1:].reshape(1, M, M, D).permute(0, 3, 1, 2)
+    patch = F.interpolate(patch, scale_factor=(float(ph + 0.1) / M, float(pw + 0.1) / M),
+                          mode="bicubic", antialias=False)
+    if tuple(patch.shape[-2:]) != (ph, pw):
+        raise ValueError(f"pos-embed interpolation produced {tuple(patch.shape[-2:])}, wanted {(ph, pw)}")
+    patch = patch.permute(0, 2, 3, 1).reshape(1, ph * pw, D)
+    return torch.cat([t[:, :1], patch], 1).numpy()
+
+
+def normalize_keys(sd: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
+    """Accept upstream checkpoints as saved (optionally 'module.'-prefixed)."""
+    out = {}
+    for k, v in sd.items():
+        if k.startswith("module."):
+            k = k[len("module."):]
+        out[k] = np.asarray(v.detach().cpu().numpy() if hasattr(v, "detach") else v, dtype=np.float32)
+    return out
+
+
+def packed_tensors(sd: Dict[str, np.ndarray], cfg: dict, img_h: int, img_w: int) -> "OrderedDict[str, np.ndarray]":
+    """The packed tensors (name -> f16/f32 numpy array) for one input size."""
+    sd = normalize_keys(sd)
+    missing = [k for k in W.expected_keys(cfg) if k not in sd and not k.endswith("mask_token")]
+    if missing:
+        raise KeyError(f"state dict lacks {len(missing)} keys, e.g. {missing[:4]}")
+    P = cfg["patch"]
+    if img_h % P or img_w % P:
+        raise ValueError(f"input size {img_h}x{img_w} is not a multiple of the patch size {P}")
+    ph, pw = img_h // P, img_w // P
+    D = cfg["embed_dim"]
+    f32 = lambda a: np.ascontiguousarray(a, dtype=np.float32).reshape(-1)  # noqa: E731
+    o: "OrderedDict[str, np.ndarray]" = OrderedDict()
+    p = "pretrained."
+    pe = sd[p + "patch_embed.proj.weight"]                   # [D,3,14,14]
+    pe16 = np.zeros((D, 3, 14, 16), np.float32)
+    pe16[..., :14] = pe
+    o["patch.w"] = _pad2(pe16.reshape(D, 3 * 14 * 16))
+    o["patch.b"] = f32(sd[p + "patch_embed.proj.bias"])
+    pos = interpolate_pos_embed(sd[p + "pos_embed"], ph, pw)
+    o["pos.patch"] = np.ascontiguousarray(pos[0, 1:], dtype=np.float32)
+    o["pos.cls"] = f32(sd[p + "cls_token"].reshape(-1) + pos[0, 0])
+    for i in range(cfg["depth"]):
+        b = f"{p}blocks.{i}."
+        q = f"b{i}."
+        o[q + "ln1.g"] = f32(sd[b + "norm1.weight"])
+        o[q + "ln1.b"] = f32(sd[b + "norm1.bias"])
+        o[q + "qkv.w"] = _pad2(sd[b + "attn.qkv.weight"])
+        o[q + "qkv.b"] = f32(sd[b + "attn.qkv.bias"])
+        o[q + "proj.w"] = _pad2(sd[b + "attn.proj.weight"])
+        o[q + "proj.b"] = f32(sd[b + "attn.proj.bias"])
+        o[q + "ls1"] = f32(sd[b + "ls1.gamma"])
+        o[q + "ln2.g"] = f32(sd[b + "norm2.weight"])
+        o[q + "ln2.b"] = f32(sd[b + "norm2.bias"])
+        o[q + "fc1.w"] = _pad2(sd[b + "mlp.fc1.weight"])
+        o[q + "fc1.b"] = f32(sd[b + "mlp.fc1.bias"])
+        o[q + "fc2.w"] = _pad2(sd[b + "mlp.fc2.weight"])
+        o[q + "fc2.b"] = f32(sd[b + "mlp.fc2.bias"])
+        o[q + "ls2"] = f32(sd[b + "ls2.gamma"])
+    o["norm.g"] = f32(sd[p + "norm.weight"])
+    o["norm.b"] = f32(sd[p + "norm.bias"])
+    h = "depth_head."
+    for i in range(4):
+        w = sd[f"{h}projects.{i}.weight"]
+        o[f"proj{i}.w"] = _pad2(w.reshape(w.shape[0], w.shape[1]))
+        o[f"proj{i}.b"] = f32(sd[f"{h}projects.{i}.bias"])
+    o["rs0.w"] = _convT(sd[h + "resize_layers.0.weight"])
+    o["rs0.b"] = f32(sd[h + "resize_layers.0.bias"])
+    o["rs1.w"] = _convT(sd[h + "resize_layers.1.weight"])
+    o["rs1.b"] = f32(sd[h + "resize_layers.1.bias"])
+    o["rs3.w"] = _conv3(sd[h + "resize_layers.3.weight"])
+    o["rs3.b"] = f32(sd[h + "resize_layers.3.bias"])
+    for i in range(4):
+        o[f"rn{i + 1}.w"] = _conv3(sd[f"{h}scratch.layer{i + 1}_rn.weight"])
+    for r in range(1, 5):
+        s = f"{h}scratch.refinenet{r}."
+        w = sd[s + "out_conv.weight"]
+        o[f"rf{r}.out.w"] = _pad2(w.reshape(w.shape[0], w.shape[1]))
+        o[f"rf{r}.out.b"] = f32(sd[s + "out_conv.bias"])
+        for u in (1, 2):
+            for c in (1, 2):
+                o[f"rf{r}.rcu{u}.c{c}.w"] = _conv3(sd[f"{s}resConfUnit{u}.conv{c}.weight"])
+                o[f"rf{r}.rcu{u}.c{c}.b"] = f32(sd[f"{s}resConfUnit{u}.conv{c}.bias"])
+    s = h + "scratch."
+    o["head.c1.w"] = _conv3(sd[s + "output_conv1.weight"])
+    o["head.c1.b"] = f32(sd[s + "output_conv1.bias"])
+    o["head.c2.w"] = _conv3(sd[s + "output_conv2.0.weight"])
+    o["head.c2.b"] = f32(sd[s + "output_conv2.0.bias"])
+    o["head.c3.w"] = f32(sd[s + "output_conv2.2.weight"])
+    o["head.c3.b"] = f32(sd[s + "output_conv2.2.bias"])
+    return o
+
+
+def _config_bytes(cfg: dict, img_h: int, img_w: int) -> bytes:
+    oc, taps = cfg["out_channels"], cfg["taps"]
+    b = struct.pack("<8i4i4i2i2f16s", cfg["embed_dim"], cfg["depth"], cfg["num_heads"], cfg["mlp_hidden"],
+                    cfg["patch"], img_h, img_w, cfg["features"], *oc, *taps, cfg["head_hidden"],
+                    1 if cfg["depth_type"] == "metric" else 0, float(cfg["max_depth"]), float(cfg["ln_eps"]),
+                    cfg["encoder"].encode()[:15])
+    assert len(b) == 96, len(b)
+    return b + b"\0" * 160
+
+
+def pack_bytes(sd: Dict[str, np.ndarray], cfg: dict, img_h: int = 518, img_w: int = 518) -> bytes:
+    tens = packed_tensors(sd, cfg, img_h, img_w)
+    n = len(tens)
+    table = bytearray()
+    data = bytearray()
+    for name, a in tens.items():
+        a = np.ascontiguousarray(a)
+        dtype = {np.dtype(np.float32): 0, np.dtype(np.float16): 1}[a.dtype]
+        if len(name) >= 80:
+            raise ValueError(f"tensor name too long: {name}")
+        dims = list(a.shape) + [0] * (4 - a.ndim)
+        off = len(data)
+        raw = a.tobytes()
+        data += raw
+        data += b"\0" * ((-len(data)) % ALIGN)
+        table += struct.pack("<80sii4iQQ8s", name.encode(), dtype, a.ndim, *dims, off, len(raw), b"")
+    head_len = 32 + 256 + len(table)
+    data_offset = -(-head_len // ALIGN) * ALIGN
+    header = struct.pack("<8sIIQQ", b"MDEPACK1", PACK_VERSION, n, data_offset, len(data))
+    blob = header + _config_bytes(cfg, img_h, img_w) + bytes(table)
+    blob += b"\0" * (data_offset - len(blob))
+    return blob + bytes(data)
+
+
+def write_packed(path: str, blob: bytes) -> str:
+    os.makedirs(os.path.dirname(os.path.abspath(path)) or ".", exist_ok=True)
+    tmp = path + ".tmp"
+    with open(tmp, "wb") as f:
+        f.write(blob)
+    os.replace(tmp, path)
+    return path
+
+
+def synthetic_blob(encoder: str = "vits", depth_type: str = "metric", img_h: int = 518, img_w: int = 518,
+                   seed: int = 1234) -> Tuple[bytes, dict]:
+    cfg = W.model_config(encoder, depth_type)
+    sd = W.synthetic_state_dict(cfg, seed)
+    return pack_bytes(sd, cfg, img_h, img_w), cfg
+
+
+def fingerprint(blob: bytes, arch: str = "gfx950") -> str:
+    return "\n".join([hashlib.sha256(blob).hexdigest(), f"packer={PACKER_VERSION}", f"arch={arch}"])

@@ -1,0 +1,128 @@
+"""End-to-end parity of the HIP engine (through the C ABI) against the oracle
+and the committed golden fixtures (HF-pinned, tests/golden/make_golden.py).
+
+Tolerance (north_star: "fp16 depth maps ... within a stated per-pixel
+tolerance"): the engine computes with fp16 operands and fp32 accumulation, so
+against the fp32 reference we require
+    rel_mean <= 0.5 %,  Pearson corr >= 0.9995,
+    per pixel |d - d_ref| <= 0.02 * max_depth (0.4 m for the metric head)
+The reference's own TensorRT fp16 engine measured rel_mean 0.170 %, max_abs
+0.0239 m, corr 0.99998 against its fp32 ONNX (reports/accuracy.json:32-35).
+Shape and index handling must be exact (output [B,H,W], tap indices, NHWC
+bookkeeping): a wrong index shows up as corr << 1.
+"""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from gpu_util import depth_metrics
+
+from monocular_depth_estimation_trt_amd import pack, weights
+from monocular_depth_estimation_trt_amd.engine import Engine
+
+pytestmark = pytest.mark.gpu
+
+REL_MEAN = 5e-3
+CORR = 0.9995
+PIX_FRAC = 0.02
+
+
+def run_engine(blob, x: np.ndarray, graph=True, max_batch=None):
+    B = x.shape[0]
+    eng = Engine.from_bytes(blob, 0, profile=((1, 3) + x.shape[2:], (B, 3) + x.shape[2:],
+                                              (max_batch or B, 3) + x.shape[2:]))
+    ctx = eng.create_execution_context()
+    ctx.set_graph_mode(graph)
+    xin = torch.from_numpy(x).cuda()
+    out = torch.empty(B, x.shape[2], x.shape[3], device="cuda")
+    ctx.set_input_shape("input", x.shape)
+    ctx.set_tensor_address("input", xin.data_ptr())
+    ctx.set_tensor_address("output", out.data_ptr())
+    ctx.execute_async_v3(torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    y = out.cpu().numpy()
+    ctx.destroy()
+    eng.destroy()
+    return y
+
+
+def check(y, ref, max_depth, what):
+    m = depth_metrics(y, ref)
+    print(what, m)
+    assert np.isfinite(y).all(), what
+    assert m["rel_mean"] <= REL_MEAN, (what, m)
+    assert m["corr"] >= CORR, (what, m)
+    assert m["max_abs"] <= PIX_FRAC * max_depth, (what, m)
+    return m
+
+
+@pytest.mark.parametrize("name", ["dav2_vits_metric_98", "dav2_vits_relative_98", "dav2_vitl_metric_98"])
+def test_engine_vs_golden_98(gpu, name):
+    z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    enc, dt = str(z["encoder"]), str(z["depth_type"])
+    cfg = weights.model_config(enc, dt)
+    sd = weights.synthetic_state_dict(cfg, int(z["seed"]))
+    assert weights.state_dict_digest(sd) == str(z["weights_sha256"]), "synthetic weight generator drifted"
+    size = int(z["size"])
+    blob = pack.pack_bytes(sd, cfg, size, size)
+    y = run_engine(blob, z["input"])
+    ref = z["output_hf"]
+    assert y.shape == ref.shape
+    md = cfg["max_depth"] if dt == "metric" else max(float(np.abs(ref).max()), 1e-3)
+    check(y, ref, md, name)
+
+
+def test_engine_vs_golden_518(gpu):
+    z = np.load(os.path.join(GOLDEN, "dav2_vits_metric_518.npz"), allow_pickle=False)
+    cfg = weights.model_config("vits", "metric")
+    sd = weights.synthetic_state_dict(cfg, 1234)
+    blob = pack.pack_bytes(sd, cfg, 518, 518)
+    x = weights.synthetic_images(1, 518, 518, first_seed=int(z["input_first_seed"]))
+    y = run_engine(blob, x)
+    assert y.shape == (1, 518, 518)
+    check(y[:, ::7, ::7], z["output_hf_sub7"], 20.0, "518 subsampled vs HF golden")
+    # full-map statistics recorded from HF
+    assert abs(float(y.mean()) - float(z["out_mean"])) < 0.01 * abs(float(z["out_mean"]))
+    assert abs(float(y.std()) - float(z["out_std"])) < 0.02 * float(z["out_std"])
+
+
+def test_engine_vs_oracle_518_full(gpu):
+    from oracle import dav2_ref
+    cfg = weights.model_config("vits", "metric")
+    sd = weights.synthetic_state_dict(cfg, 1234)
+    x = weights.synthetic_images(2, 518, 518, first_seed=0)
+    ref = dav2_ref.forward(dav2_ref.to_torch(sd), cfg, x).numpy()
+    y = run_engine(pack.pack_bytes(sd, cfg, 518, 518), x)
+    check(y, ref, 20.0, "518 B=2 vs oracle")
+
+
+def test_engine_nonsquare_vs_oracle(gpu):
+    """126x182 (9x13 patches): pos-embed interpolation, odd 4th-scale size."""
+    from oracle import dav2_ref
+    cfg = weights.model_config("vits", "metric")
+    sd = weights.synthetic_state_dict(cfg, 99)
+    x = weights.synthetic_images(2, 126, 182, first_seed=3)
+    ref = dav2_ref.forward(dav2_ref.to_torch(sd), cfg, x).numpy()
+    y = run_engine(pack.pack_bytes(sd, cfg, 126, 182), x)
+    assert y.shape == (2, 126, 182)
+    check(y, ref, 20.0, "126x182 vs oracle")
+
+
+def test_batch_and_graph_consistency(gpu):
+    cfg = weights.model_config("vits", "metric")
+    sd = weights.synthetic_state_dict(cfg, 5)
+    blob = pack.pack_bytes(sd, cfg, 98, 98)
+    x = weights.synthetic_images(3, 98, 98, first_seed=11)
+    y3 = run_engine(blob, x, graph=True)
+    y3e = run_engine(blob, x, graph=False)
+    assert np.array_equal(y3, y3e), "graph replay must equal eager launches bit for bit"
+    y3b = run_engine(blob, x, graph=True)
+    assert np.array_equal(y3, y3b), "engine must be deterministic"
+    for i in range(3):
+        yi = run_engine(blob, x[i:i + 1], max_batch=4)
+        m = depth_metrics(yi, y3[i:i + 1])
+        assert m["max_abs"] < 0.05 and m["rel_mean"] < 1e-3, (i, m)

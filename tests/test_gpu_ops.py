@@ -1,0 +1,243 @@
+"""Per-kernel parity: each HIP kernel (through the C ABI) vs a plain PyTorch
+fp32 CPU reference of the same op, on seeded inputs.  Shapes are chosen to hit
+tails (M, N, K not tile multiples), both tile configurations, and the DA-V2
+shapes where they are cheap.
+
+Tolerances: operands are fp16 and accumulation fp32, outputs rounded to fp16,
+so |err| <= atol + rtol*|ref| with rtol = 1e-2, atol scaled to the output
+magnitude (stated per test).
+"""
+
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from gpu_util import close, conv_w, nchw, nhwc, op, pad_w, ptr, stream
+
+pytestmark = pytest.mark.gpu
+
+G = torch.Generator().manual_seed(7)
+
+
+def rn(*shape, scale=1.0):
+    return torch.randn(*shape, generator=G) * scale
+
+
+def f16(t, dev):
+    return t.half().to(dev)
+
+
+@pytest.mark.parametrize("m,n,k,act", [(300, 200, 96, 0), (1370, 1152, 384, 0), (777, 1536, 384, 2),
+                                       (64, 48, 48, 1), (5, 32, 64, 1), (2048, 384, 1536, 0)])
+def test_linear(gpu, m, n, k, act):
+    a, w, b = rn(m, k), rn(n, k, scale=k ** -0.5), rn(n, scale=0.1)
+    a16, w16 = a.half().float(), w.half().float()
+    ref = a16 @ w16.T + b
+    if act == 1:
+        ref = F.relu(ref)
+    elif act == 2:
+        ref = F.gelu(ref)
+    wp = pad_w(w).to(gpu)
+    out = torch.empty(m, n, dtype=torch.float16, device=gpu)
+    op("mde_op_linear", ptr(f16(a, gpu)), k, ptr(wp), wp.shape[1], m, n, k, ptr(b.to(gpu)), act, ptr(out), n,
+       stream())
+    close(out, ref, 1e-2, 1e-2, f"linear {m}x{n}x{k} act{act}")
+
+
+def test_linear_residual(gpu):
+    m, n, k = 1370, 384, 1536
+    a, w, b = rn(m, k), rn(n, k, scale=k ** -0.5), rn(n, scale=0.1)
+    ls = 0.5 + 0.05 * rn(n)
+    x = rn(m, n)
+    ref = x + ls * (a.half().float() @ w.half().float().T + b)
+    xg = x.clone().to(gpu)
+    wp = pad_w(w).to(gpu)
+    op("mde_op_linear_residual", ptr(f16(a, gpu)), k, ptr(wp), wp.shape[1], m, n, k, ptr(b.to(gpu)),
+       ptr(ls.to(gpu)), ptr(xg), n, stream())
+    close(xg, ref, 2e-3, 2e-3, "linear_residual")
+
+
+def test_qkv_layout(gpu):
+    B, T, H = 2, 50, 6
+    D = 64 * H
+    Tp = 64
+    a, w, b = rn(B * T, D), rn(3 * D, D, scale=D ** -0.5), rn(3 * D, scale=0.1)
+    full = a.half().float() @ w.half().float().T + b                         # [B*T, 3D]
+    full = full.reshape(B, T, 3, H, 64)
+    wp = pad_w(w).to(gpu)
+    q = torch.zeros(B * H, Tp, 64, dtype=torch.float16, device=gpu)
+    k = torch.zeros_like(q)
+    vt = torch.zeros(B * H, 64, Tp, dtype=torch.float16, device=gpu)
+    op("mde_op_qkv", ptr(f16(a, gpu)), ptr(wp), wp.shape[1], ptr(b.to(gpu)), B, T, H, Tp, 0.125, ptr(q), ptr(k),
+       ptr(vt), stream())
+    rq = full[:, :, 0].permute(0, 2, 1, 3).reshape(B * H, T, 64) * 0.125
+    rk = full[:, :, 1].permute(0, 2, 1, 3).reshape(B * H, T, 64)
+    rv = full[:, :, 2].permute(0, 2, 3, 1).reshape(B * H, 64, T)
+    close(q[:, :T], rq, 1e-2, 1e-2, "q")
+    close(k[:, :T], rk, 1e-2, 1e-2, "k")
+    close(vt[:, :, :T], rv, 1e-2, 1e-2, "vt")
+    assert float(q[:, T:].abs().max()) == 0 and float(vt[:, :, T:].abs().max()) == 0, "pad must stay zero"
+
+
+@pytest.mark.parametrize("B,H,T", [(2, 6, 50), (1, 6, 1370), (1, 2, 64), (3, 1, 65), (1, 16, 130)])
+def test_attention(gpu, B, H, T):
+    Tp = -(-T // 64) * 64
+    q = rn(B * H, T, 64) * 0.125 * 2.0
+    k = rn(B * H, T, 64) * 2.0
+    v = rn(B * H, T, 64)
+    qh, kh, vh = q.half().float(), k.half().float(), v.half().float()
+    p = torch.softmax(qh @ kh.transpose(1, 2), dim=-1)
+    ref = (p @ vh).reshape(B, H, T, 64).permute(0, 2, 1, 3).reshape(B * T, H * 64)
+    qg = torch.zeros(B * H, Tp, 64, dtype=torch.float16, device=gpu)
+    kg = torch.zeros_like(qg)
+    vtg = torch.zeros(B * H, 64, Tp, dtype=torch.float16, device=gpu)
+    qg[:, :T] = q.half().to(gpu)
+    kg[:, :T] = k.half().to(gpu)
+    vtg[:, :, :T] = v.transpose(1, 2).half().to(gpu)
+    o = torch.empty(B * T, H * 64, dtype=torch.float16, device=gpu)
+    op("mde_op_attention", ptr(qg), ptr(kg), ptr(vtg), ptr(o), B, H, T, Tp, H * 64, stream())
+    close(o, ref, 2e-2, 5e-3, f"attention B{B} H{H} T{T}")
+
+
+def test_attention_spiky_rows(gpu):
+    """Force the online-softmax rescale: one key dominates late in the row."""
+    B, H, T = 1, 2, 300
+    Tp = 320
+    q = rn(B * H, T, 64) * 0.1
+    k = rn(B * H, T, 64)
+    k[:, 290] = q[:, :].mean(1) * 60.0                 # huge score for key 290 (last tile)
+    k[:, 5] = q[:, :].mean(1) * 30.0                   # large early key
+    v = rn(B * H, T, 64)
+    qh, kh, vh = q.half().float(), k.half().float(), v.half().float()
+    ref = (torch.softmax(qh @ kh.transpose(1, 2), -1) @ vh).reshape(B, H, T, 64).permute(0, 2, 1, 3)
+    ref = ref.reshape(B * T, H * 64)
+    qg = torch.zeros(B * H, Tp, 64, dtype=torch.float16, device=gpu)
+    kg = torch.zeros_like(qg)
+    vtg = torch.zeros(B * H, 64, Tp, dtype=torch.float16, device=gpu)
+    qg[:, :T], kg[:, :T], vtg[:, :, :T] = q.half().to(gpu), k.half().to(gpu), v.transpose(1, 2).half().to(gpu)
+    o = torch.empty(B * T, H * 64, dtype=torch.float16, device=gpu)
+    op("mde_op_attention", ptr(qg), ptr(kg), ptr(vtg), ptr(o), B, H, T, Tp, H * 64, stream())
+    close(o, ref, 2e-2, 5e-3, "attention spiky")
+
+
+@pytest.mark.parametrize("D,skip", [(384, 0), (384, 1), (1024, 0), (768, 1)])
+def test_layernorm(gpu, D, skip):
+    B, T = 2, 50
+    x = rn(B * T, D) * 3 + 1.5
+    g, b = 1 + 0.1 * rn(D), 0.02 * rn(D)
+    ref = F.layer_norm(x, (D,), g, b, 1e-6)
+    if skip:
+        ref = ref.reshape(B, T, D)[:, 1:].reshape(B * (T - 1), D)
+    y = torch.empty(ref.shape, dtype=torch.float16, device=gpu)
+    op("mde_op_layernorm", ptr(x.to(gpu)), ptr(y), ptr(g.to(gpu)), ptr(b.to(gpu)), B * T, D, 1e-6, T, skip,
+       stream())
+    close(y, ref, 1e-2, 1e-2, f"layernorm D{D} skip{skip}")
+
+
+@pytest.mark.parametrize("B,Hh,Ww", [(2, 98, 98), (1, 126, 182)])
+def test_patch_embed(gpu, B, Hh, Ww):
+    D = 384
+    ph, pw = Hh // 14, Ww // 14
+    img = rn(B, 3, Hh, Ww)
+    w, b = rn(D, 3, 14, 14, scale=588 ** -0.5), rn(D, scale=0.02)
+    pos, cls_pos = rn(ph * pw, D, scale=0.5), rn(D, scale=0.5)
+    t = F.conv2d(img.half().float(), w.half().float(), b, stride=14).flatten(2).transpose(1, 2) + pos
+    ref = torch.cat([cls_pos.expand(B, 1, D), t], 1).reshape(B * (ph * pw + 1), D)
+    w16 = torch.zeros(D, 3, 14, 16)
+    w16[..., :14] = w
+    wp = pad_w(w16.reshape(D, 672)).to(gpu)
+    scratch = torch.empty(B * ph * pw, 672, dtype=torch.float16, device=gpu)
+    x = torch.empty(B * (ph * pw + 1), D, device=gpu)
+    op("mde_op_patch_embed", ptr(img.to(gpu)), B, Hh, Ww, ptr(wp), wp.shape[1], ptr(b.to(gpu)), ptr(pos.to(gpu)),
+       ptr(cls_pos.to(gpu)), D, ptr(scratch), ptr(x), stream())
+    close(x, ref, 1e-3, 2e-3, "patch_embed")
+
+
+@pytest.mark.parametrize("B,h,w,cin,cout,stride,relu_in,act,nres", [
+    (2, 19, 19, 64, 64, 1, 1, 1, 0), (1, 37, 37, 64, 64, 1, 0, 0, 2), (1, 37, 37, 384, 384, 2, 0, 0, 0),
+    (1, 74, 74, 96, 64, 1, 0, 0, 0), (2, 28, 28, 48, 64, 1, 0, 0, 1), (1, 148, 148, 64, 32, 1, 0, 1, 0),
+    (1, 7, 7, 256, 256, 2, 0, 0, 0)])
+def test_conv3x3(gpu, B, h, w, cin, cout, stride, relu_in, act, nres):
+    x = rn(B, cin, h, w)
+    wt, b = rn(cout, cin, 3, 3, scale=(9 * cin) ** -0.5), rn(cout, scale=0.02)
+    xin = x.half().float()
+    ref = F.conv2d(F.relu(xin) if relu_in else xin, wt.half().float(), b, stride=stride, padding=1)
+    if act == 1:
+        ref = F.relu(ref)
+    res = [rn(*ref.shape) for _ in range(nres)]
+    for r in res:
+        ref = ref + r.half().float()
+    wp = conv_w(wt).to(gpu)
+    ho, wo = ref.shape[2], ref.shape[3]
+    out = torch.empty(B, ho, wo, cout, dtype=torch.float16, device=gpu)
+    rg = [nhwc(r).half().to(gpu) for r in res] + [None, None]
+    op("mde_op_conv3x3", ptr(nhwc(x).half().to(gpu)), B, h, w, cin, ptr(wp), wp.shape[1], cout, stride, relu_in,
+       ptr(b.to(gpu)), act, ptr(rg[0]), ptr(rg[1]), ptr(out), stream())
+    close(nchw(out), ref, 1e-2, 1e-2, f"conv3x3 {h}x{w} {cin}->{cout} s{stride}")
+
+
+@pytest.mark.parametrize("B,sh,sw,uh,uw,cin,cout", [(1, 10, 10, 19, 19, 64, 32), (2, 16, 12, 28, 21, 32, 64),
+                                                    (1, 148, 148, 296, 296, 64, 32)])
+def test_conv3x3_up(gpu, B, sh, sw, uh, uw, cin, cout):
+    x = rn(B, cin, sh, sw)
+    wt, b = rn(cout, cin, 3, 3, scale=(9 * cin) ** -0.5), rn(cout, scale=0.02)
+    up = F.interpolate(x.half().float(), size=(uh, uw), mode="bilinear", align_corners=True).half().float()
+    ref = F.conv2d(up, wt.half().float(), b, padding=1)
+    wp = conv_w(wt).to(gpu)
+    out = torch.empty(B, uh, uw, cout, dtype=torch.float16, device=gpu)
+    op("mde_op_conv3x3_up", ptr(nhwc(x).half().to(gpu)), B, sh, sw, cin, uh, uw, ptr(wp), wp.shape[1], cout,
+       ptr(b.to(gpu)), 0, ptr(out), stream())
+    close(nchw(out), ref, 1e-2, 1.5e-2, "conv3x3_up")
+
+
+@pytest.mark.parametrize("s,cin", [(4, 48), (2, 96), (4, 256)])
+def test_conv_transpose(gpu, s, cin):
+    B, h, w = 2, 7, 9
+    cout = cin
+    x = rn(B, cin, h, w)
+    wt, b = rn(cin, cout, s, s, scale=cin ** -0.5), rn(cout, scale=0.02)
+    ref = F.conv_transpose2d(x.half().float(), wt.half().float(), b, stride=s)
+    wp = pad_w(wt.permute(2, 3, 1, 0).reshape(s * s * cout, cin)).to(gpu)
+    out = torch.empty(B, h * s, w * s, cout, dtype=torch.float16, device=gpu)
+    op("mde_op_conv_transpose", ptr(nhwc(x).half().to(gpu)), B, h, w, cin, ptr(wp), wp.shape[1], cout, s,
+       ptr(b.to(gpu)), ptr(out), stream())
+    close(nchw(out), ref, 1e-2, 1e-2, f"convT s{s}")
+
+
+@pytest.mark.parametrize("ih,iw,oh,ow,c", [(19, 19, 37, 37, 64), (37, 37, 74, 74, 64), (148, 148, 296, 296, 64),
+                                           (4, 4, 7, 7, 256), (5, 7, 1, 9, 16), (296, 296, 518, 518, 32)])
+def test_resize(gpu, ih, iw, oh, ow, c):
+    B = 2
+    x = rn(B, c, ih, iw)
+    ref = F.interpolate(x.half().float(), size=(oh, ow), mode="bilinear", align_corners=True)
+    out = torch.empty(B, oh, ow, c, dtype=torch.float16, device=gpu)
+    op("mde_op_resize_bilinear", ptr(nhwc(x).half().to(gpu)), B, ih, iw, c, oh, ow, ptr(out), stream())
+    close(nchw(out), ref, 1e-2, 1e-2, "resize")
+
+
+@pytest.mark.parametrize("metric", [1, 0])
+def test_depth_head(gpu, metric):
+    B, sh, sw, uh, uw, cin = 2, 24, 24, 42, 42, 32
+    x = rn(B, cin, sh, sw)
+    w1, b1 = rn(32, cin, 3, 3, scale=(9 * cin) ** -0.5), rn(32, scale=0.02)
+    w2, b2 = rn(32, scale=32 ** -0.5), 0.05
+    up = F.interpolate(x.half().float(), size=(uh, uw), mode="bilinear", align_corners=True).half().float()
+    h = F.relu(F.conv2d(up, w1.half().float(), b1, padding=1))
+    z = (h * w2.view(1, 32, 1, 1)).sum(1) + b2
+    ref = torch.sigmoid(z) * 20.0 if metric else F.relu(z)
+    wp = conv_w(w1).to(gpu)
+    out = torch.empty(B, uh, uw, device=gpu)
+    op("mde_op_depth_head", ptr(nhwc(x).half().to(gpu)), B, sh, sw, cin, uh, uw, ptr(wp), wp.shape[1],
+       ptr(b1.to(gpu)), ptr(w2.to(gpu)), b2, metric, 20.0, ptr(out), stream())
+    close(out, ref, 1e-2, 2e-2, "depth_head")
+
+
+def test_bad_arguments_raise(gpu):
+    from monocular_depth_estimation_trt_amd._lib import MDEError
+    with pytest.raises(MDEError):
+        op("mde_op_linear", ptr(None), 8, ptr(None), 32, 4, 4, 8, ptr(None), 0, ptr(None), 4, stream())
+    x = torch.zeros(64, device=gpu, dtype=torch.float16)
+    with pytest.raises(MDEError):  # K not a multiple of 8
+        op("mde_op_linear", ptr(x), 7, ptr(x), 32, 1, 1, 7, ptr(None), 0, ptr(x), 1, stream())
