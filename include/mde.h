@@ -131,8 +131,8 @@ int mde_rt_event_elapsed_ms(float* ms, void* start, void* end);
 
 /* ---- kernel-level entry points ---------------------------------------- */
 /* All tensors are device pointers.  f16 = IEEE half.  Weights W are
- * [Npad][ldw] f16 row-major (K contiguous), rows >= N zero, ldw % 32 == 0,
- * ldw >= K rounded up to 32, Npad a multiple of 128.  Activation maps are
+ * [Npad][ldw] f16 row-major (K contiguous), rows >= N zero, ldw % 64 == 0,
+ * ldw >= K rounded up to 64, Npad a multiple of 128; N % 8 == 0.  Activation maps are
  * NHWC f16.  act: 0 none, 1 ReLU, 2 GELU(erf). */
 int mde_op_layernorm(const float* x, void* y_f16, const float* gamma, const float* beta, int rows, int dim,
                      float eps, int tokens, int skip_cls, void* stream);

@@ -20,7 +20,7 @@ INCLUDE = os.path.join(ROOT, "include")
 LIB = os.path.join(HERE, "libmde_hip.so")
 OBJDIR = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("MDE_OFFLOAD_ARCH", "gfx950")
-SOURCES = ["gemm.hip", "attention.hip", "elementwise.hip", "engine.hip"]
+SOURCES = ["gemm.hip", "conv.hip", "attention.hip", "elementwise.hip", "engine.hip"]
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
          "-Wno-unused-result", "-I", CSRC, "-I", INCLUDE]
 
@@ -55,15 +55,22 @@ def up_to_date() -> bool:
         return f.read().strip() == _digest()
 
 
-def build_library(force: bool = False, verbose: bool = True) -> str:
-    if not force and up_to_date():
+def build_library(force: bool = False, verbose: bool = True, out: str = "", defines=()) -> str:
+    """Build the library; `out`/`defines` build a tuning variant elsewhere
+    (e.g. defines=("MDE_GEMM_BK=32",)) without touching the product .so."""
+    variant = bool(out or defines)
+    if not variant and not force and up_to_date():
         return LIB
     cc = hipcc()
-    os.makedirs(OBJDIR, exist_ok=True)
+    objdir = OBJDIR if not variant else os.path.join(OBJDIR, "variant_" + hashlib.sha1(
+        (out + "|".join(defines)).encode()).hexdigest()[:10])
+    os.makedirs(objdir, exist_ok=True)
+    dflags = [f"-D{d}" for d in defines]
+    target = out or LIB
 
     def compile_one(src: str) -> str:
-        obj = os.path.join(OBJDIR, src + ".o")
-        cmd = [cc, *FLAGS, "-c", os.path.join(CSRC, src), "-o", obj]
+        obj = os.path.join(objdir, src + ".o")
+        cmd = [cc, *FLAGS, *dflags, "-c", os.path.join(CSRC, src), "-o", obj]
         r = subprocess.run(cmd, capture_output=True, text=True)
         if r.returncode != 0:
             raise RuntimeError(f"hipcc failed on {src}:\n{r.stderr[-6000:]}")
@@ -71,17 +78,18 @@ def build_library(force: bool = False, verbose: bool = True) -> str:
 
     with cf.ThreadPoolExecutor(max_workers=min(len(SOURCES), os.cpu_count() or 4)) as ex:
         objs = list(ex.map(compile_one, SOURCES))
-    tmp = LIB + ".tmp"
+    tmp = target + ".tmp"
     cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, *objs]
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr[-6000:]}")
-    os.replace(tmp, LIB)
-    with open(_stamp_path(), "w") as f:
-        f.write(_digest())
+    os.replace(tmp, target)
+    if not variant:
+        with open(_stamp_path(), "w") as f:
+            f.write(_digest())
     if verbose:
-        print(f"[mde] built {LIB}", file=sys.stderr)
-    return LIB
+        print(f"[mde] built {target}", file=sys.stderr)
+    return target
 
 
 if __name__ == "__main__":

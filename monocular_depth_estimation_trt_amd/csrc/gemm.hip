@@ -13,67 +13,135 @@
 // LayerScale+residual, a12 fc1+GELU/fc2, a14 projects, a15 resize_layers,
 // a16 layerN_rn, a17 RCU convs + out_conv, a18/a19 head convs.
 //
-// Tiling: BM x BN x 32 block tile, WM x WN waves, each wave owns
-// (BM/WM) x (BN/WN) as 16x16 MFMA tiles.  Operands are register-staged into
-// a double-buffered LDS image (one barrier per K-step) with 64-byte rows and
-// the chunk swizzle c ^ ((row>>1)&3), which makes every ds_read_b128 lane
-// group of the fragment reads conflict-free.
+// Structure (cdna_hip_programming.md section 5, "step-3 structure"):
+//  * BM x BN x 64 block tile, WM x WN waves (4), each wave (BM/WM) x (BN/WN)
+//    as 16x16 MFMA tiles, two 32-deep MFMA k-substeps per K-step;
+//  * operands staged global -> LDS with global_load_lds_dwordx4 (no VGPR
+//    round trip), two LDS stages, one barrier per K-step; LDS rows are 128 B
+//    (64 halves) with chunk swizzle c ^ (row & 7) applied on the SOURCE
+//    address (the LDS image is lane-linear) and on the fragment read, which
+//    makes the ds_read_b128 fragment reads conflict-free;
+//  * implicit-im2col A: each lane computes its own source pixel; padding
+//    taps read a zero line (a glds lane can't be masked, it can be redirected);
+//  * the bilinear-upsampled conv A (A_CONV3_UP) is register-staged because
+//    every element is a 4-tap blend;
+//  * MFMA issued with W as the A operand, so each lane owns 4 consecutive
+//    output columns of one row: the fused epilogue (tile_epilogue.h) stores
+//    8 B (f16) / 16 B (f32) per lane straight from the accumulators.
+#include <cstdlib>
+
 #include "mde_device.h"
 #include "mde_ops.h"
+#include "tile_epilogue.h"
+
+#ifndef MDE_GEMM_BK
+#define MDE_GEMM_BK 64
+#endif
 
 namespace mde {
 
 namespace {
 
-constexpr int BK = 32;
+__device__ __attribute__((aligned(64))) f16 g_zero_line[64];  // zero-initialised module global
 
-MDE_DEV int swz(int row, int chunk) { return (chunk ^ ((row >> 1) & 3)) * 8; }
+MDE_DEV void glds16(const void* src, void* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds(src, lds_wave_base, 16, 0, 0);
+}
 
-template <int BM, int BN, int WM, int WN, int AM, int EM>
+MDE_DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+// LDS tile geometry for a K-step of BK halves: rows of BK*2 bytes, 16-byte
+// chunks; one glds wave-instruction (64 lanes x 16 B) fills RW rows.
+template <int BK>
+struct KGeo {
+  static constexpr int ROWB = BK * 2;       // bytes per row
+  static constexpr int CH = BK / 8;         // chunks per row
+  static constexpr int RW = 64 / CH;        // rows per wave-instruction
+  // physical chunk of logical chunk lc in row r (conflict-free ds_read_b128)
+  static MDE_DEV int pch(int r, int lc) {
+    if constexpr (BK == 64) return lc ^ (r & 7);
+    else return lc ^ ((r >> 1) & 3);
+  }
+};
+
+template <int BM, int BN, int BK, int WM, int WN, int AM, int EM>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) {
-  constexpr int NT = WM * WN * 64;
+  using G = KGeo<BK>;
+  constexpr int ROWB = G::ROWB, CH = G::CH;
+  constexpr int NW = WM * WN;
+  constexpr int NT = NW * 64;
   constexpr int TM = BM / (WM * 16);
   constexpr int TN = BN / (WN * 16);
   static_assert(TM * WM * 16 == BM && TN * WN * 16 == BN, "tile");
-  constexpr int RSTEP = NT / 4;               // rows covered by one pass of the block
-  constexpr int AL = (BM + RSTEP - 1) / RSTEP;  // A chunks per thread
-  constexpr int BL = (BN + RSTEP - 1) / RSTEP;  // B chunks per thread
-  constexpr int STAGE = (BM + BN) * BK;
-  __shared__ __attribute__((aligned(16))) f16 lds[2 * STAGE];
+  // glds wave-instructions per tile (each fills RW rows); wave w issues
+  // instructions w, w + NW, ... (APASS / BPASS slots, the last maybe partial)
+  constexpr int AINS = BM / G::RW, BINS = BN / G::RW;
+  static_assert(AINS * G::RW == BM && BINS * G::RW == BN, "tile rows vs glds rows");
+  constexpr int APASS = (AINS + NW - 1) / NW, BPASS = (BINS + NW - 1) / NW;
+  constexpr int STAGE = (BM + BN) * ROWB;
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
   const int ntn = (p.N + BN - 1) / BN;
   const int tm = blockIdx.x / ntn, tn = blockIdx.x - tm * ntn;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kc = tid & 3;      // 16-byte chunk column this thread stages
-  const int rbase = tid >> 2;  // first row this thread stages
 
-  // ---- A-row state (fixed over the K loop) ----
-  const f16* arow[AL];
-  int iy0[AL], ix0[AL];
-  bool rv[AL];
+  // ---- glds lane geometry: lane -> (row within a wave-instruction, chunk)
+  const int lrow = lane / CH;
+  const int lch = G::pch(lrow, lane % CH);  // logical chunk (involution: pch(pch(c)) = c)
+
+  // ---- A operand state ----
+  const f16* arow[APASS];
+  int iy0[APASS], ix0[APASS];
+  bool rv[APASS];
+  if constexpr (AM != A_CONV3_UP) {
 #pragma unroll
-  for (int i = 0; i < AL; ++i) {
-    const int r = rbase + i * RSTEP;
-    const int gm = m0 + r;
-    rv[i] = (r < BM) && (gm < p.M);
-    const int gmc = rv[i] ? gm : 0;
-    if constexpr (AM == A_DENSE) {
-      arow[i] = reinterpret_cast<const f16*>(p.A) + (size_t)gmc * p.lda;
-      iy0[i] = ix0[i] = 0;
-    } else {
+    for (int i = 0; i < APASS; ++i) {
+      const int r = (wave + i * NW) * G::RW + lrow;
+      const int gm = m0 + r;
+      rv[i] = gm < p.M;
+      const int gmc = rv[i] ? gm : (p.M - 1);
+      if constexpr (AM == A_DENSE) {
+        arow[i] = reinterpret_cast<const f16*>(p.A) + (size_t)gmc * p.lda;
+        iy0[i] = ix0[i] = 0;
+      } else {
+        const int hw = p.oh * p.ow;
+        const int b = gmc / hw;
+        const int rem = gmc - b * hw;
+        const int oy = rem / p.ow, ox = rem - (rem / p.ow) * p.ow;
+        iy0[i] = oy * p.stride - 1;
+        ix0[i] = ox * p.stride - 1;
+        arow[i] = reinterpret_cast<const f16*>(p.A) + (size_t)b * p.ch * p.cw * p.cc;
+      }
+    }
+  }
+  // register-staged A (A_CONV3_UP): thread -> 16B chunks (row, logical chunk)
+  constexpr int UPC = (AM == A_CONV3_UP) ? (BM * CH) / NT : 1;
+  static_assert(AM != A_CONV3_UP || (BM * CH) % NT == 0, "up-conv staging");
+  const f16* urow[UPC];
+  int uy0[UPC], ux0[UPC];
+  bool uv[UPC];
+  const int ulch = tid % CH;
+  if constexpr (AM == A_CONV3_UP) {
+#pragma unroll
+    for (int i = 0; i < UPC; ++i) {
+      const int r = tid / CH + i * (NT / CH);
+      const int gm = m0 + r;
+      uv[i] = gm < p.M;
+      const int gmc = uv[i] ? gm : 0;
       const int hw = p.oh * p.ow;
       const int b = gmc / hw;
       const int rem = gmc - b * hw;
       const int oy = rem / p.ow, ox = rem - (rem / p.ow) * p.ow;
-      iy0[i] = oy * p.stride - 1;
-      ix0[i] = ox * p.stride - 1;
-      arow[i] = reinterpret_cast<const f16*>(p.A) + (size_t)b * p.ch * p.cw * p.cc;
+      uy0[i] = oy - 1;
+      ux0[i] = ox - 1;
+      urow[i] = reinterpret_cast<const f16*>(p.A) + (size_t)b * p.ch * p.cw * p.cc;
     }
   }
-  // conv: (tap, c0) of k = k0 + kc*8, advanced by BK per step
-  int tap = 0, c0 = kc * 8;
+  // conv K position (tap, c0) of this lane's chunk, advanced by BK per step
+  int tap = 0, c0 = (AM == A_CONV3_UP ? ulch : lch) * 8;
   if constexpr (AM != A_DENSE) {
     while (c0 >= p.cc) { c0 -= p.cc; ++tap; }
   }
@@ -83,58 +151,59 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) 
     usx = p.uw > 1 ? (float)(p.cw - 1) / (float)(p.uw - 1) : 0.f;
   }
 
-  const f16* wrow[BL];
-  bool bv[BL];
-#pragma unroll
-  for (int i = 0; i < BL; ++i) {
-    const int r = rbase + i * RSTEP;
-    bv[i] = r < BN;
-    wrow[i] = reinterpret_cast<const f16*>(p.W) + (size_t)(n0 + (bv[i] ? r : 0)) * p.ldw;
-  }
+  // ---- B operand (weights [Npad][ldw], ldw % 64 == 0) ----
+  const f16* wbase = reinterpret_cast<const f16*>(p.W) + (size_t)(n0 + wave * G::RW + lrow) * p.ldw + lch * 8;
+  auto aslot = [&](int i) { return (wave + i * NW) * G::RW * ROWB; };  // LDS row offset of slot i
 
-  f16x8 ra[AL], rb[BL];
+  f16x8 ru[UPC];
 
-  auto fetch = [&](int k0) {
-    const int k = k0 + kc * 8;
-    const bool kv = k < p.K;
+  auto issue = [&](int kt, int buf) {
+    char* sbase = smem + buf * STAGE;
+    const int k0 = kt * BK;
 #pragma unroll
-    for (int i = 0; i < AL; ++i) {
-      f16x8 v = zero8();
-      if constexpr (AM == A_DENSE) {
-        if (rv[i] && kv) v = *reinterpret_cast<const f16x8*>(arow[i] + k);
-      } else {
-        const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+    for (int i = 0; i < BPASS; ++i)
+      if (BINS % NW == 0 || wave + i * NW < BINS)
+        glds16(wbase + (size_t)i * NW * G::RW * p.ldw + k0, sbase + BM * ROWB + aslot(i));
+    if constexpr (AM == A_DENSE) {
+      const int k = k0 + lch * 8;
+      const int kk = k < p.K ? k : 0;  // K tail: W is zero there, any finite A will do
+#pragma unroll
+      for (int i = 0; i < APASS; ++i)
+        if (AINS % NW == 0 || wave + i * NW < AINS) glds16(arow[i] + kk, sbase + aslot(i));
+    } else if constexpr (AM == A_CONV3) {
+      const bool kv = (k0 + lch * 8) < p.K;
+      const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+#pragma unroll
+      for (int i = 0; i < APASS; ++i) {
         const int iy = iy0[i] + ky, ix = ix0[i] + kx;
-        if constexpr (AM == A_CONV3) {
-          if (rv[i] && kv && iy >= 0 && iy < p.ch && ix >= 0 && ix < p.cw)
-            v = *reinterpret_cast<const f16x8*>(arow[i] + ((size_t)iy * p.cw + ix) * p.cc + c0);
-        } else {  // A_CONV3_UP: virtual map = bilinear(align_corners) upsample to uh x uw
-          if (rv[i] && kv && iy >= 0 && iy < p.uh && ix >= 0 && ix < p.uw) {
-            const float fy = usy * (float)iy, fx = usx * (float)ix;
-            const int y0 = (int)fy, x0 = (int)fx;
-            const int y1 = y0 + (y0 < p.ch - 1 ? 1 : 0), x1 = x0 + (x0 < p.cw - 1 ? 1 : 0);
-            const float ly1 = fy - (float)y0, ly0 = 1.f - ly1;
-            const float lx1 = fx - (float)x0, lx0 = 1.f - lx1;
-            const f16* base = arow[i] + c0;
-            const f16x8 a = *reinterpret_cast<const f16x8*>(base + ((size_t)y0 * p.cw + x0) * p.cc);
-            const f16x8 b = *reinterpret_cast<const f16x8*>(base + ((size_t)y0 * p.cw + x1) * p.cc);
-            const f16x8 c = *reinterpret_cast<const f16x8*>(base + ((size_t)y1 * p.cw + x0) * p.cc);
-            const f16x8 d = *reinterpret_cast<const f16x8*>(base + ((size_t)y1 * p.cw + x1) * p.cc);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-              const float t = ly0 * (lx0 * (float)a[j] + lx1 * (float)b[j]) +
-                              ly1 * (lx0 * (float)c[j] + lx1 * (float)d[j]);
-              v[j] = (f16)t;
-            }
-          }
-        }
-        if (p.relu_in) v = relu8(v);
+        const bool ok = rv[i] && kv && iy >= 0 && iy < p.ch && ix >= 0 && ix < p.cw;
+        const f16* src = ok ? arow[i] + ((size_t)iy * p.cw + ix) * p.cc + c0 : g_zero_line;
+        if (AINS % NW == 0 || wave + i * NW < AINS) glds16(src, sbase + aslot(i));
       }
-      ra[i] = v;
-    }
+    } else {  // A_CONV3_UP: blend 4 taps of the source map in registers
+      const bool kv = (k0 + ulch * 8) < p.K;
+      const int ky = tap / 3, kx = tap - (tap / 3) * 3;
 #pragma unroll
-    for (int i = 0; i < BL; ++i) {
-      if (bv[i]) rb[i] = *reinterpret_cast<const f16x8*>(wrow[i] + k);
+      for (int i = 0; i < UPC; ++i) {
+        f16x8 v = zero8();
+        const int iy = uy0[i] + ky, ix = ux0[i] + kx;
+        if (uv[i] && kv && iy >= 0 && iy < p.uh && ix >= 0 && ix < p.uw) {
+          const float fy = usy * (float)iy, fx = usx * (float)ix;
+          const int y0 = (int)fy, x0 = (int)fx;
+          const int y1 = y0 + (y0 < p.ch - 1 ? 1 : 0), x1 = x0 + (x0 < p.cw - 1 ? 1 : 0);
+          const float ly1 = fy - (float)y0, ly0 = 1.f - ly1;
+          const float lx1 = fx - (float)x0, lx0 = 1.f - lx1;
+          const f16* base = urow[i] + c0;
+          const f16x8 a = *reinterpret_cast<const f16x8*>(base + ((size_t)y0 * p.cw + x0) * p.cc);
+          const f16x8 b = *reinterpret_cast<const f16x8*>(base + ((size_t)y0 * p.cw + x1) * p.cc);
+          const f16x8 c = *reinterpret_cast<const f16x8*>(base + ((size_t)y1 * p.cw + x0) * p.cc);
+          const f16x8 d = *reinterpret_cast<const f16x8*>(base + ((size_t)y1 * p.cw + x1) * p.cc);
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+            v[j] = (f16)(ly0 * (lx0 * (float)a[j] + lx1 * (float)b[j]) + ly1 * (lx0 * (float)c[j] + lx1 * (float)d[j]));
+        }
+        ru[i] = v;
+      }
     }
     if constexpr (AM != A_DENSE) {
       c0 += BK;
@@ -142,21 +211,20 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) 
     }
   };
 
-  auto stash = [&](int buf) {
-    f16* sA = lds + buf * STAGE;
-    f16* sB = sA + BM * BK;
+  auto commit_up = [&](int buf) {
+    if constexpr (AM == A_CONV3_UP) {
+      char* sA = smem + buf * STAGE;
 #pragma unroll
-    for (int i = 0; i < AL; ++i) {
-      const int r = rbase + i * RSTEP;
-      if (r < BM) *reinterpret_cast<f16x8*>(sA + r * BK + swz(r, kc)) = ra[i];
-    }
-#pragma unroll
-    for (int i = 0; i < BL; ++i) {
-      const int r = rbase + i * RSTEP;
-      if (bv[i]) *reinterpret_cast<f16x8*>(sB + r * BK + swz(r, kc)) = rb[i];
+      for (int i = 0; i < UPC; ++i) {
+        const int r = tid / CH + i * (NT / CH);
+        *reinterpret_cast<f16x8*>(sA + r * ROWB + G::pch(r, ulch) * 16) = ru[i];
+      }
     }
   };
 
+  // acc[i][j] holds C^T for the 16x16 block (m-block i, n-block j): the MFMA is
+  // issued with W as its A operand, so lane l owns row m = .. + (l & 15) and the
+  // four consecutive columns n = .. + 4(l >> 4) + r -- stores are 8/16 B wide.
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -164,139 +232,59 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) 
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = (p.K + BK - 1) / BK;
-  fetch(0);
-  stash(0);
+  issue(0, 0);
+  commit_up(0);
+  wait_vm();
   __syncthreads();
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) fetch((kt + 1) * BK);
-    const f16* sA = lds + cur * STAGE;
-    const f16* sB = sA + BM * BK;
-    f16x8 fa[TM], fb[TN];
+    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+    const char* sA = smem + cur * STAGE;
+    const char* sB = sA + BM * ROWB;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int r = wm * TM * 16 + i * 16 + (lane & 15);
-      fa[i] = *reinterpret_cast<const f16x8*>(sA + r * BK + swz(r, lane >> 4));
+    for (int s = 0; s < BK / 32; ++s) {
+      f16x8 fa[TM], fb[TN];
+      const int lc = 4 * s + (lane >> 4);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int r = wm * TM * 16 + i * 16 + (lane & 15);
+        fa[i] = *reinterpret_cast<const f16x8*>(sA + r * ROWB + G::pch(r, lc) * 16);
+        if constexpr (AM == A_CONV3) {
+          if (p.relu_in) fa[i] = relu8(fa[i]);
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int r = wn * TN * 16 + j * 16 + (lane & 15);
+        fb[j] = *reinterpret_cast<const f16x8*>(sB + r * ROWB + G::pch(r, lc) * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);
     }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int r = wn * TN * 16 + j * 16 + (lane & 15);
-      fb[j] = *reinterpret_cast<const f16x8*>(sB + r * BK + swz(r, lane >> 4));
-    }
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fa[i], fb[j], acc[i][j]);
-    if (kt + 1 < nk) stash(cur ^ 1);
+    if (kt + 1 < nk) commit_up(cur ^ 1);
+    wait_vm();
     __syncthreads();
   }
 
-  // ---- epilogue ----
-  const int mrow0 = m0 + wm * TM * 16 + (lane >> 4) * 4;
-  const int ncol0 = n0 + wn * TN * 16 + (lane & 15);
-
-  if constexpr (EM == E_HEAD) {
-    static_assert(BN == 32 && WN == 1 && TN == 2, "head epilogue needs the full 32-channel row");
+  // ---- epilogue: lane owns (m, n..n+3) per block ----
+  int mrow[TM];
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        float part = 0.f;
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int n = j * 16 + (lane & 15);
-          const float v = acc[i][j][r] + p.bias[n];
-          part += (v > 0.f ? v : 0.f) * p.w2[n];
-        }
-        part += __shfl_xor(part, 1, 64);
-        part += __shfl_xor(part, 2, 64);
-        part += __shfl_xor(part, 4, 64);
-        part += __shfl_xor(part, 8, 64);
-        const int m = mrow0 + i * 16 + r;
-        if ((lane & 15) == 0 && m < p.M) {
-          const float z = part + p.b2;
-          p.out32[m] = p.head_metric ? p.max_depth / (1.f + __expf(-z)) : (z > 0.f ? z : 0.f);
-        }
-      }
-    }
-    return;
-  } else {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int n = ncol0 + j * 16;
-      if (n >= p.N) continue;
-      const float bn = p.bias ? p.bias[n] : 0.f;
-      // per-column constants of the scatter epilogues
-      int qwhich = 0, qh = 0, qd = 0;
-      int cq = 0, cco = 0, cdy = 0, cdx = 0;
-      float lsn = 0.f;
-      if constexpr (EM == E_QKV) {
-        const int D = p.heads * 64;
-        qwhich = n / D;
-        const int w = n - qwhich * D;
-        qh = w >> 6;
-        qd = w & 63;
-      }
-      if constexpr (EM == E_CONVT) {
-        cq = n / p.cout;
-        cco = n - cq * p.cout;
-        cdy = cq / p.s;
-        cdx = cq - cdy * p.s;
-      }
-      if constexpr (EM == E_RESID) lsn = p.ls[n];
-      const float bconv = (EM == E_CONVT) ? p.bias[cco] : bn;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const int m = mrow0 + i * 16 + r;
-          if (m >= p.M) continue;
-          float v = acc[i][j][r];
-          if constexpr (EM == E_STORE) {
-            v += bn;
-            if (p.act == ACT_RELU) v = v > 0.f ? v : 0.f;
-            else if (p.act == ACT_GELU) v = gelu_erf(v);
-            const size_t o = (size_t)m * p.ldo + n;
-            if (p.res0) v += (float)reinterpret_cast<const f16*>(p.res0)[o];
-            if (p.res1) v += (float)reinterpret_cast<const f16*>(p.res1)[o];
-            reinterpret_cast<f16*>(p.out16)[o] = (f16)v;
-          } else if constexpr (EM == E_QKV) {
-            v += bn;
-            const int b = m / p.T, t = m - (m / p.T) * p.T;
-            const size_t bh = (size_t)b * p.heads + qh;
-            if (qwhich == 0)
-              reinterpret_cast<f16*>(p.q)[(bh * p.Tpad + t) * 64 + qd] = (f16)(v * p.qscale);
-            else if (qwhich == 1)
-              reinterpret_cast<f16*>(p.k)[(bh * p.Tpad + t) * 64 + qd] = (f16)v;
-            else
-              reinterpret_cast<f16*>(p.vt)[(bh * 64 + qd) * p.Tpad + t] = (f16)v;
-          } else if constexpr (EM == E_RESID) {
-            float* x = p.x32 + (size_t)m * p.ldo + n;
-            *x = *x + lsn * (v + bn);
-          } else if constexpr (EM == E_PATCH) {
-            const int b = m / p.npatch, pi = m - (m / p.npatch) * p.npatch;
-            p.x32[((size_t)b * p.T + 1 + pi) * p.ldo + n] = v + bn + p.pos[(size_t)pi * p.ldo + n];
-          } else if constexpr (EM == E_CONVT) {
-            const int hw = p.ih * p.iw;
-            const int b = m / hw, rem = m - (m / hw) * hw;
-            const int y = rem / p.iw, x = rem - (rem / p.iw) * p.iw;
-            const int OH = p.ih * p.s, OW = p.iw * p.s;
-            const size_t o = (((size_t)b * OH + y * p.s + cdy) * OW + x * p.s + cdx) * p.cout + cco;
-            reinterpret_cast<f16*>(p.out16)[o] = (f16)(v + bconv);
-          }
-        }
-      }
-    }
+  for (int i = 0; i < TM; ++i) {
+    const int m = m0 + wm * TM * 16 + i * 16 + (lane & 15);
+    mrow[i] = m < p.M ? m : -1;
   }
+  store_tile<EM, TM, TN>(p, acc, mrow, n0 + wn * TN * 16 + (lane >> 4) * 4, lane);
 }
-
 template <int BM, int BN, int WM, int WN, int AM, int EM>
 hipError_t run(const GemmParams& p, hipStream_t st) {
   const int gm = (p.M + BM - 1) / BM, gn = (p.N + BN - 1) / BN;
   const long long blocks = (long long)gm * gn;
   if (blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, WM, WN, AM, EM>), dim3((unsigned)blocks),
-                     dim3(WM * WN * 64), 0, st, p);
+  constexpr int BKSEL = MDE_GEMM_BK;
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, BKSEL, WM, WN, AM, EM>), dim3((unsigned)blocks), dim3(WM * WN * 64), 0,
+                     st, p);
   return hipGetLastError();
 }
 
@@ -318,13 +306,27 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
   }
 }
 
+// MDE_CONV_IM2COL=1 forces the implicit-im2col GEMM path for 3x3 convs (A/B aid).
+bool getenv_im2col() {
+  static const int v = [] {
+    const char* e = getenv("MDE_CONV_IM2COL");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  return v != 0;
+}
+
 }  // namespace
 
 hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
   if (p.M <= 0 || p.N <= 0) return hipSuccess;
-  if (p.K <= 0 || (p.K & 7) || (p.ldw & 31) || p.ldw < ((p.K + 31) / 32) * 32) return hipErrorInvalidValue;
+  if (p.K <= 0 || (p.K & 7) || (p.N & 7) || (p.ldw & 63) || p.ldw < ((p.K + 63) / 64) * 64)
+    return hipErrorInvalidValue;
+  if (p.amode == A_DENSE && ((p.lda & 7) || p.lda < p.K)) return hipErrorInvalidValue;
   if (p.amode != A_DENSE && (p.cc & 7)) return hipErrorInvalidValue;
+  if ((p.emode == E_STORE || p.emode == E_RESID || p.emode == E_PATCH) && (p.ldo & 7)) return hipErrorInvalidValue;
+  if (p.emode == E_CONVT && (p.cout & 7)) return hipErrorInvalidValue;
   if (p.emode == E_HEAD && (p.N != 32 || p.amode == A_DENSE)) return hipErrorInvalidValue;
+  if (p.amode != A_DENSE && conv_direct_supported(p) && !getenv_im2col()) return launch_conv3(p, st);
   switch (p.amode) {
     case A_DENSE:
       switch (p.emode) {

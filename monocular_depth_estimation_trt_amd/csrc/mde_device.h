@@ -24,7 +24,19 @@ MDE_DEV float wave_sum(float v) {
   return v;
 }
 
-MDE_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// erf by Abramowitz & Stegun 7.1.26 (|error| <= 1.5e-7, below f16 rounding):
+// one exp + one reciprocal instead of the libm polynomial ladder.
+MDE_DEV float erf_fast(float x) {
+  const float ax = fabsf(x);
+  const float t = __frcp_rn(1.0f + 0.3275911f * ax);
+  const float poly = ((((1.061405429f * t - 1.453152027f) * t + 1.421413741f) * t - 0.284496736f) * t +
+                      0.254829592f) * t;
+  const float y = 1.0f - poly * __expf(-ax * ax);
+  return copysignf(y, x);
+}
+
+// GELU with the exact-erf definition (nn.GELU() default, upstream DINOv2 Mlp).
+MDE_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
 
 MDE_DEV f16x8 zero8() {
   f16x8 z;

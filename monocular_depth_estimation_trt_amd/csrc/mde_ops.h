@@ -30,7 +30,7 @@ struct GemmParams {
   int amode = A_DENSE, emode = E_STORE;
   int M = 0, N = 0, K = 0;
   const h16* A = nullptr; int lda = 0;
-  const h16* W = nullptr; int ldw = 0;  // weights [Npad][ldw], ldw % 32 == 0
+  const h16* W = nullptr; int ldw = 0;  // weights [Npad][ldw], ldw % 64 == 0
   // conv geometry: source NHWC map [cb][ch][cw][cc]; output map [cb][oh][ow]
   int cb = 0, ch = 0, cw = 0, cc = 0;
   int uh = 0, uw = 0;  // virtual (upsampled) input size, A_CONV3_UP
@@ -54,6 +54,11 @@ struct GemmParams {
 };
 
 hipError_t launch_gemm(const GemmParams& p, hipStream_t st);
+
+// Direct 3x3 conv with an LDS halo patch (conv.hip); launch_gemm routes
+// A_CONV3 / A_CONV3_UP problems here when conv_direct_supported().
+bool conv_direct_supported(const GemmParams& p);
+hipError_t launch_conv3(const GemmParams& p, hipStream_t st);
 
 hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T,
                             int Tpad, int ldo, hipStream_t st);

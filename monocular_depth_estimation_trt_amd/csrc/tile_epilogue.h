@@ -1,0 +1,127 @@
+// Shared MFMA-tile epilogue of the GEMM and the direct-conv kernels.
+//
+// acc[i][j] holds C^T of the 16x16 block (row block i, column block j): the
+// MFMA is issued with the weights as its A operand, so lane l owns output row
+// mrow[i] (= -1 when outside the problem) and the four consecutive columns
+// ncol + 16 j .. +3 -- every store is 8 B (f16) or 16 B (f32) per lane.
+// The epilogue fuses what follows the contraction in the reference graph.
+#pragma once
+#include "mde_device.h"
+#include "mde_ops.h"
+
+namespace mde {
+
+template <int EM, int TM, int TN>
+MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&mrow)[TM], int ncol, int lane) {
+    if constexpr (EM == E_HEAD) {
+    static_assert(TN == 2, "head epilogue needs the full 32-channel row in one wave (BN 32, WN 1)");
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      float part = 0.f;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const int n = j * 16 + (lane >> 4) * 4 + r;
+          const float v = acc[i][j][r] + p.bias[n];
+          part += (v > 0.f ? v : 0.f) * p.w2[n];
+        }
+      part += __shfl_xor(part, 16, 64);
+      part += __shfl_xor(part, 32, 64);
+      const int m = mrow[i];
+      if ((lane >> 4) == 0 && m >= 0) {
+        const float z = part + p.b2;
+        p.out32[m] = p.head_metric ? p.max_depth / (1.f + __expf(-z)) : (z > 0.f ? z : 0.f);
+      }
+    }
+    return;
+  } else {
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = ncol + j * 16;
+      if (n >= p.N) continue;
+      float4 bn = {0.f, 0.f, 0.f, 0.f};
+      if constexpr (EM == E_CONVT) {
+        bn = *reinterpret_cast<const float4*>(p.bias + (n % p.cout));
+      } else {
+        if (p.bias) bn = *reinterpret_cast<const float4*>(p.bias + n);
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int m = mrow[i];
+        if (m < 0) continue;
+        float v[4] = {acc[i][j][0] + bn.x, acc[i][j][1] + bn.y, acc[i][j][2] + bn.z, acc[i][j][3] + bn.w};
+        if constexpr (EM == E_STORE) {
+          if (p.act == ACT_RELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+          } else if (p.act == ACT_GELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
+          }
+          const size_t o = (size_t)m * p.ldo + n;
+          if (p.res0) {
+            const f16x4 r0 = *reinterpret_cast<const f16x4*>(reinterpret_cast<const f16*>(p.res0) + o);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += (float)r0[r];
+          }
+          if (p.res1) {
+            const f16x4 r1 = *reinterpret_cast<const f16x4*>(reinterpret_cast<const f16*>(p.res1) + o);
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] += (float)r1[r];
+          }
+          f16x4 h;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h[r] = (f16)v[r];
+          *reinterpret_cast<f16x4*>(reinterpret_cast<f16*>(p.out16) + o) = h;
+        } else if constexpr (EM == E_QKV) {
+          const int D = p.heads * 64;
+          const int which = n / D, w = n - which * D;
+          const int b = m / p.T, t = m - (m / p.T) * p.T;
+          const size_t bh = (size_t)b * p.heads + (w >> 6);
+          if (which == 2) {
+            f16* dst = reinterpret_cast<f16*>(p.vt) + (bh * 64 + (w & 63)) * p.Tpad + t;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) dst[(size_t)r * p.Tpad] = (f16)v[r];
+          } else {
+            const float sc = which == 0 ? p.qscale : 1.f;
+            f16x4 h;
+#pragma unroll
+            for (int r = 0; r < 4; ++r) h[r] = (f16)(v[r] * sc);
+            f16* dst = (which == 0 ? reinterpret_cast<f16*>(p.q) : reinterpret_cast<f16*>(p.k)) +
+                       (bh * p.Tpad + t) * 64 + (w & 63);
+            *reinterpret_cast<f16x4*>(dst) = h;
+          }
+        } else if constexpr (EM == E_RESID) {
+          float4* x = reinterpret_cast<float4*>(p.x32 + (size_t)m * p.ldo + n);
+          const float4 l = *reinterpret_cast<const float4*>(p.ls + n);
+          float4 xv = *x;
+          xv.x += l.x * v[0];
+          xv.y += l.y * v[1];
+          xv.z += l.z * v[2];
+          xv.w += l.w * v[3];
+          *x = xv;
+        } else if constexpr (EM == E_PATCH) {
+          const int b = m / p.npatch, pi = m - (m / p.npatch) * p.npatch;
+          const float4 ps = *reinterpret_cast<const float4*>(p.pos + (size_t)pi * p.ldo + n);
+          *reinterpret_cast<float4*>(p.x32 + ((size_t)b * p.T + 1 + pi) * p.ldo + n) =
+              float4{v[0] + ps.x, v[1] + ps.y, v[2] + ps.z, v[3] + ps.w};
+        } else if constexpr (EM == E_CONVT) {
+          const int q = n / p.cout, co = n - q * p.cout;
+          const int dy = q / p.s, dx = q - (q / p.s) * p.s;
+          const int hw = p.ih * p.iw;
+          const int b = m / hw, rem = m - (m / hw) * hw;
+          const int y = rem / p.iw, x = rem - (rem / p.iw) * p.iw;
+          const int OH = p.ih * p.s, OW = p.iw * p.s;
+          const size_t o = (((size_t)b * OH + y * p.s + dy) * OW + x * p.s + dx) * p.cout + co;
+          f16x4 h;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) h[r] = (f16)v[r];
+          *reinterpret_cast<f16x4*>(reinterpret_cast<f16*>(p.out16) + o) = h;
+        }
+      }
+    }
+  }
+}
+
+}  // namespace mde

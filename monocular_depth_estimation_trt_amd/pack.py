@@ -6,7 +6,7 @@ and `run.py build` -> `core/common.py:166-274` (TensorRT builder) -- with one
 deterministic host-side pass that lays the weights out for the gfx950 kernels:
 
 * every matrix operand becomes f16 [Npad][Kpad] (K contiguous; N padded to a
-  multiple of 128 and K to a multiple of 32 with zeros) -- the B-operand
+  multiple of 128 and K to a multiple of 64 with zeros) -- the B-operand
   layout of the MFMA GEMM (csrc/gemm.hip);
 * 3x3 conv weights [Cout][Cin][3][3] -> [Cout][ky][kx][Cin] (the implicit
   im2col K order over an NHWC map);
@@ -40,7 +40,7 @@ PACKER_VERSION = "mde-pack-1"
 ALIGN = 256
 
 
-def _pad2(a: np.ndarray, n_mult: int = 128, k_mult: int = 32) -> np.ndarray:
+def _pad2(a: np.ndarray, n_mult: int = 128, k_mult: int = 64) -> np.ndarray:
     n, k = a.shape
     N = -(-n // n_mult) * n_mult
     K = -(-k // k_mult) * k_mult
@@ -50,7 +50,7 @@ def _pad2(a: np.ndarray, n_mult: int = 128, k_mult: int = 32) -> np.ndarray:
 
 
 def _conv3(w: np.ndarray) -> np.ndarray:
-    """[Cout][Cin][3][3] -> f16 [Cout_pad][9*Cin pad32] in (ky, kx, ci) order."""
+    """[Cout][Cin][3][3] -> f16 [Cout_pad][9*Cin pad64] in (ky, kx, ci) order."""
     co, ci, kh, kw = w.shape
     assert kh == 3 and kw == 3, w.shape
     return _pad2(np.ascontiguousarray(w.transpose(0, 2, 3, 1)).reshape(co, 9 * ci))

@@ -35,7 +35,7 @@ def op(name: str, *args) -> None:
         _KEEP.clear()
 
 
-def pad_w(w: torch.Tensor, n_mult: int = 128, k_mult: int = 32) -> torch.Tensor:
+def pad_w(w: torch.Tensor, n_mult: int = 128, k_mult: int = 64) -> torch.Tensor:
     """[N][K] -> f16 [Npad][Kpad] zero-padded device tensor (the packer's layout)."""
     n, k = w.shape
     N = -(-n // n_mult) * n_mult

@@ -1,0 +1,106 @@
+"""Time the hot-path kernels at DA-V2 shapes (rank-0 tuning aid, GPU box).
+
+    python tools/bench_kernels.py [--batch 32] [--lib path/to/libmde_hip.so]
+
+Each op is launched through the C ABI on torch's current stream and timed
+with torch.cuda.Event over `--iters` back-to-back launches (after warmup).
+TF/s uses the algorithmic FLOP of that launch.
+"""
+import argparse
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--lib", default="")
+    ap.add_argument("--only", default="")
+    a = ap.parse_args()
+    if a.lib:
+        os.environ["MDE_LIB"] = a.lib
+    import torch
+    from gpu_util import conv_w, pad_w, ptr, stream
+    from monocular_depth_estimation_trt_amd import _lib
+    dev = torch.device("cuda:0")
+    B, T, D, H = a.batch, 1370, 384, 6
+    M = B * T
+    g = torch.Generator(device=dev).manual_seed(0)
+
+    def rnd(*s, scale=1.0, dtype=torch.float16):
+        return (torch.randn(*s, generator=g, device=dev) * scale).to(dtype)
+
+    def timeit(name, fn, flop):
+        if a.only and a.only not in name:
+            return
+        for _ in range(3):
+            fn()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(a.iters):
+            fn()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / a.iters
+        print(f"{name:28s} {ms * 1e3:9.1f} us  {flop / ms / 1e9:8.1f} TF/s", flush=True)
+
+    L = _lib.lib()
+    st = stream()
+    x16 = rnd(M, 4 * D)
+    out = torch.empty(M, 4 * D, dtype=torch.float16, device=dev)
+    x32 = torch.randn(M, D, device=dev)
+    bias = torch.randn(4 * D, device=dev) * 0.02
+    ls = torch.full((4 * D,), 0.5, device=dev)
+    for name, n, k, act in (("qkv-like N1152 K384", 3 * D, D, 0), ("fc1 N1536 K384 gelu", 4 * D, D, 2),
+                            ("fc1 N1536 K384 nogelu", 4 * D, D, 0)):
+        w = pad_w(rnd(n, k, scale=k ** -0.5))
+        timeit(name, lambda: L.mde_op_linear(ptr(x16), k, ptr(w), w.shape[1], M, n, k, ptr(bias), act, ptr(out),
+                                             n, st), 2.0 * M * n * k)
+    for name, n, k in (("proj N384 K384 resid", D, D), ("fc2 N384 K1536 resid", D, 4 * D)):
+        w = pad_w(rnd(n, k, scale=k ** -0.5))
+        timeit(name, lambda: L.mde_op_linear_residual(ptr(x16), k, ptr(w), w.shape[1], M, n, k, ptr(bias), ptr(ls),
+                                                      ptr(x32), D, st), 2.0 * M * n * k)
+    Tp = 1408
+    w = pad_w(rnd(3 * D, D, scale=D ** -0.5))
+    q = torch.zeros(B * H, Tp, 64, dtype=torch.float16, device=dev)
+    k_ = torch.zeros_like(q)
+    vt = torch.zeros(B * H, 64, Tp, dtype=torch.float16, device=dev)
+    timeit("qkv N1152 K384 (E_QKV)", lambda: L.mde_op_qkv(ptr(x16), ptr(w), w.shape[1], ptr(bias), B, T, H, Tp,
+                                                        0.125, ptr(q), ptr(k_), ptr(vt), st), 2.0 * M * 3 * D * D)
+    q.normal_()
+    k_.normal_()
+    vt.normal_()
+    o = torch.empty(M, D, dtype=torch.float16, device=dev)
+    timeit("attention T1370 H6", lambda: L.mde_op_attention(ptr(q), ptr(k_), ptr(vt), ptr(o), B, H, T, Tp, D, st),
+           4.0 * B * H * T * T * 64)
+    F = 64
+    for hw in (148, 74):
+        xin = rnd(B, hw, hw, F)
+        w = conv_w(rnd(F, F, 3, 3, scale=(9 * F) ** -0.5).float())
+        oc = torch.empty(B, hw, hw, F, dtype=torch.float16, device=dev)
+        timeit(f"rcu conv3x3 {hw}^2 64->64", lambda: L.mde_op_conv3x3(ptr(xin), B, hw, hw, F, ptr(w), w.shape[1], F,
+                                                                    1, 1, ptr(bias), 1, ptr(None), ptr(None),
+                                                                    ptr(oc), st), 2.0 * B * hw * hw * F * F * 9)
+    xin = rnd(B, 148, 148, F)
+    w = conv_w(rnd(32, F, 3, 3, scale=(9 * F) ** -0.5).float())
+    oc = torch.empty(B, 296, 296, 32, dtype=torch.float16, device=dev)
+    timeit("head conv1 up148->296 64->32", lambda: L.mde_op_conv3x3_up(ptr(xin), B, 148, 148, F, 296, 296, ptr(w),
+                                                                       w.shape[1], 32, ptr(bias), 0, ptr(oc), st),
+           2.0 * B * 296 * 296 * 32 * F * 9)
+    xin = rnd(B, 296, 296, 32)
+    w = conv_w(rnd(32, 32, 3, 3, scale=(9 * 32) ** -0.5).float())
+    w2 = torch.randn(32, device=dev) * 0.2
+    od = torch.empty(B, 518, 518, device=dev)
+    timeit("head conv2 up296->518 +1x1", lambda: L.mde_op_depth_head(ptr(xin), B, 296, 296, 32, 518, 518, ptr(w),
+                                                                     w.shape[1], ptr(bias), ptr(w2), 0.1, 1, 20.0,
+                                                                     ptr(od), st), 2.0 * B * 518 * 518 * 32 * 32 * 9)
+
+
+if __name__ == "__main__":
+    main()
