@@ -142,6 +142,10 @@ int mde_op_linear_residual(const void* a_f16, int lda, const void* w_f16, int ld
                            const float* bias, const float* layer_scale, float* x32, int ldx, void* stream);
 int mde_op_qkv(const void* a_f16, const void* w_f16, int ldw, const float* bias, int batch, int tokens,
                int heads, int tokens_pad, float q_scale, void* q_f16, void* k_f16, void* vt_f16, void* stream);
+/* q pre-multiplied by dh^-0.5 * log2(e) (scores in log2 units, as mde_op_qkv writes with
+ * q_scale = 0.125 * log2(e)); k/q [B*H][tokens_pad][64], vt [B*H][64][tokens_pad] with key t
+ * stored at column vt_pos(t) = (t & ~31) | ((t & 15) >> 2) << 3 | ((t & 31) >> 4) << 2 | (t & 3)
+ * (the layout mde_op_qkv writes). */
 int mde_op_attention(const void* q_f16, const void* k_f16, const void* vt_f16, void* o_f16, int batch, int heads,
                      int tokens, int tokens_pad, int ldo, void* stream);
 int mde_op_patch_embed(const float* img, int batch, int h, int w, const void* w_f16, int ldw, const float* bias,

@@ -3,19 +3,30 @@
 // upstream `Attention.forward`: softmax(q*dh^-0.5 @ k^T) @ v).
 //
 // Layouts (written by the qkv GEMM epilogue, E_QKV):
-//   q, k : [B*H][Tpad][64] f16, q already multiplied by dh^-0.5 = 1/8 (exact)
-//   vt   : [B*H][64][Tpad] f16 (v transposed), pad columns t >= T are zero
+//   q, k : [B*H][Tpad][64] f16, q pre-multiplied by dh^-0.5 * log2(e), so the
+//          scores come out in log2 units and exp() is one v_exp_f32 (exp2)
+//   vt   : [B*H][64][Tpad] f16 (v transposed; key t stored at vt_pos(t), a
+//          permutation inside each 32-key group), pad columns t >= T zero
 //   o    : [B*T][ldo] f16, head h in columns h*64 .. h*64+63
 //
-// One workgroup = 4 waves = 64 queries of one (batch, head); each wave owns 16
-// queries.  The score tile is computed TRANSPOSED, S^T = K Q^T, so the MFMA
-// accumulator holds a key x query block whose query sits on the lane: the
-// online-softmax max/sum over keys is a reduction over registers plus two
-// lane shuffles (xor 16, 32), and P^T feeds the P.V MFMA as the B operand
-// straight from the accumulator (O^T = V^T P^T) with no LDS round trip.
-// K and V^T key tiles (64 keys) are register-staged into a double-buffered
-// LDS image with conflict-free swizzles (K: chunk ^ (row&7) for ds_read_b128;
-// V^T: chunk ^ ((row>>1)&7) for ds_read_b64).  Softmax statistics are fp32.
+// Structure.  A workgroup = NW waves; a wave owns QW (16 or 32) queries as
+// 16-query column blocks.  The score tile is computed TRANSPOSED, S^T = K Q^T,
+// so the query sits on the MFMA lane: the online-softmax max / sum over keys
+// is a reduction over the lane's registers plus two lane shuffles (xor 16,
+// 32), and P^T feeds the P.V MFMA as the B operand straight from the
+// accumulators (O^T = V^T P^T), no LDS round trip.  K and V^T key tiles (64
+// keys) stream global -> LDS by global_load_lds through a 3-slot ring, two
+// tiles in flight, counted `s_waitcnt vmcnt` + raw s_barrier (a
+// __syncthreads() would drain the DMA).  LDS images are lane-linear with the
+// swizzle chunk ^ (row & 7) applied on the source address (conflict-free
+// ds_read_b128 for both).  The running max rides in the score MFMA's C
+// operand (S' = QK^T - m), so the softmax is max-check + exp2 + sum per
+// element; O and l are rescaled only when a max grows.  Softmax statistics in
+// fp32; keys >= T are masked on the last tile only.
+#include <cstdlib>
+#include <cstring>
+#include <type_traits>
+
 #include "mde_device.h"
 #include "mde_ops.h"
 
@@ -23,174 +34,268 @@ namespace mde {
 
 namespace {
 
-constexpr int KT = 64;  // keys per tile
-constexpr float LOG2E = 1.4426950408889634f;
+constexpr int KT = 64;        // keys per tile
+constexpr int TILE_B = KT * 128;  // bytes of one K (or V^T) tile image: 64 rows x 128 B
 
 typedef f16 f16x4v __attribute__((ext_vector_type(4)));
 
-MDE_DEV int kswz(int row, int chunk) { return row * 64 + ((chunk ^ (row & 7)) << 3); }
-MDE_DEV int vswz(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 1) & 7)) << 3); }
+// byte offset of 16-B chunk `chunk` of a 128-B row: conflict-free ds_read_b128
+MDE_DEV int kswz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
-__global__ void __launch_bounds__(256) attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k,
-                                                        const f16* __restrict__ vt, f16* __restrict__ o,
-                                                        int H, int T, int Tpad, int ldo) {
-  __shared__ __attribute__((aligned(16))) f16 sK[2][KT * 64];
-  __shared__ __attribute__((aligned(16))) f16 sV[2][64 * KT];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+// max / sum over the 4 lanes {l, l^16, l^32, l^48} with VALU lane swaps
+// (v_permlane16/32_swap) instead of LDS-routed shuffles
+MDE_DEV float xmax4(float x) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+  auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r2[0]), __uint_as_float(r2[1]));
+}
+MDE_DEV float xsum4(float x) {
+  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = __uint_as_float(r[0]) + __uint_as_float(r[1]);
+  auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r2[0]) + __uint_as_float(r2[1]);
+}
+
+template <int N>
+MDE_DEV void wait_vm_n() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Workgroup barrier that leaves LDS-DMA in flight: own LDS reads retired,
+// raw s_barrier, and compiler fences so no LDS access moves across it.
+MDE_DEV void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+template <int QW, int NW>
+__global__ void __launch_bounds__(NW * 64) attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k,
+                                                           const f16* __restrict__ vt, f16* __restrict__ o, int H,
+                                                           int T, int Tpad, int ldo) {
+  constexpr int NQ = QW / 16;            // 16-query blocks per wave
+  constexpr int BQ = QW * NW;            // queries per workgroup
+  constexpr int INS = 8 / NW;            // glds instructions per wave per image (8 per 64-row image)
+  constexpr int PER_TILE = 2 * INS;      // K + V^T
+  constexpr int SLOT = 2 * TILE_B;
+  static_assert(8 % NW == 0, "waves must divide the 8 glds instructions of a tile");
+  __shared__ __attribute__((aligned(16))) char smem[3 * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int bh = blockIdx.y;
   const int b = bh / H, h = bh - (bh / H) * H;
-  const int qbase = blockIdx.x * 64 + wave * 16;
+  const int qbase = blockIdx.x * BQ + wave * QW;
   const int l15 = lane & 15, hq = lane >> 4;
 
   const f16* qb = q + (size_t)bh * Tpad * 64;
   const f16* kb = k + (size_t)bh * Tpad * 64;
   const f16* vb = vt + (size_t)bh * 64 * Tpad;
 
-  // Q^T fragments (B operand): lane holds Q[q = qbase + l15][32s + 8hq + j]
-  f16x8 qf[2];
+  // Q^T fragments (B operand): lane holds Q[q][32s + 8hq + j] of its query column
+  f16x8 qf[NQ][2];
 #pragma unroll
-  for (int s = 0; s < 2; ++s)
-    qf[s] = *reinterpret_cast<const f16x8*>(qb + (size_t)(qbase + l15) * 64 + 32 * s + 8 * hq);
-
-  // staging: 512 chunks of 16B per tile for K and for V^T; 2 + 2 per thread
-  f16x8 rk[2], rv[2];
-  auto fetch = [&](int kt) {
+  for (int c = 0; c < NQ; ++c)
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + i * 256;
-      const int row = c >> 3, ch = c & 7;
-      rk[i] = *reinterpret_cast<const f16x8*>(kb + (size_t)(kt * KT + row) * 64 + ch * 8);
-      rv[i] = *reinterpret_cast<const f16x8*>(vb + (size_t)row * Tpad + kt * KT + ch * 8);
+    for (int s = 0; s < 2; ++s) {
+      const int qi = qbase + c * 16 + l15;
+      qf[c][s] = qi < Tpad ? *reinterpret_cast<const f16x8*>(qb + (size_t)qi * 64 + 32 * s + 8 * hq) : zero8();
     }
-  };
-  auto stash = [&](int buf) {
+
+  // glds geometry: lane -> row lrow of an 8-row group, physical chunk lane & 7
+  const int lrow = lane >> 3, pc = lane & 7;
+  auto issue = [&](int kt, int slot) {
+    char* sK = smem + slot * SLOT;
+    char* sV = sK + TILE_B;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int c = tid + i * 256;
-      const int row = c >> 3, ch = c & 7;
-      *reinterpret_cast<f16x8*>(&sK[buf][kswz(row, ch)]) = rk[i];
-      *reinterpret_cast<f16x8*>(&sV[buf][vswz(row, ch)]) = rv[i];
+    for (int i = 0; i < INS; ++i) {
+      const int g = wave * INS + i;  // 8-row group 0..7
+      const int row = g * 8 + lrow;
+      const int kch = pc ^ (row & 7);
+      __builtin_amdgcn_global_load_lds(kb + (size_t)(kt * KT + row) * 64 + kch * 8, sK + g * 8 * 128, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(vb + (size_t)row * Tpad + kt * KT + kch * 8, sV + g * 8 * 128, 16, 0, 0);
     }
   };
 
-  float m_run = -INFINITY;  // running max (log2 domain) of this lane's query
-  float l_run = 0.f;        // this lane's partial row sum (its 16 key rows per tile)
-  f32x4 acc[4];
+  // running max per query (log2 units) as an MFMA C operand: every tile after
+  // the first computes S' = S - m_run directly in the accumulator, so
+  // p = exp2(S') needs no subtraction unless some max grew (rare branch)
+  float m_run[NQ], l_run[NQ];
+  f32x4 negm[NQ];
+  f32x4 acc[NQ][4];
 #pragma unroll
-  for (int d = 0; d < 4; ++d) acc[d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int c = 0; c < NQ; ++c) {
+    m_run[c] = 0.f;
+    l_run[c] = 0.f;
+    negm[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int d = 0; d < 4; ++d) acc[c][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
 
   const int nkt = (T + KT - 1) / KT;
-  fetch(0);
-  stash(0);
-  __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nkt) fetch(kt + 1);
-    const f16* K_ = sK[cur];
-    const f16* V_ = sV[cur];
+  issue(0, 0);
+  if (nkt > 1) {
+    issue(1, 1);
+    wait_vm_n<PER_TILE>();
+  } else {
+    wait_vm_n<0>();
+  }
+  lds_barrier();
 
-    // S^T[key][query] for 4 key sub-tiles of 16
-    f32x4 s[4];
+  auto tile = [&](int kt, int slot, auto first_tag) {
+    constexpr bool FIRST = decltype(first_tag)::value;
+    const char* K_ = smem + slot * SLOT;
+    const char* V_ = K_ + TILE_B;
+    // S'^T[key][query] = K Q^T - m_run: 4 key sub-tiles x NQ query blocks
+    f32x4 s[NQ][4];
 #pragma unroll
     for (int t4 = 0; t4 < 4; ++t4) {
-      s[t4] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int row = t4 * 16 + l15;
+      const f16x8 k0 = *reinterpret_cast<const f16x8*>(K_ + kswz(row, hq));
+      const f16x8 k1 = *reinterpret_cast<const f16x8*>(K_ + kswz(row, 4 + hq));
 #pragma unroll
-      for (int ss = 0; ss < 2; ++ss) {
-        const f16x8 kf = *reinterpret_cast<const f16x8*>(K_ + kswz(row, 4 * ss + hq));
-        s[t4] = mfma16x16x32(kf, qf[ss], s[t4]);
+      for (int c = 0; c < NQ; ++c) {
+        s[c][t4] = mfma16x16x32(k0, qf[c][0], FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : negm[c]);
+        s[c][t4] = mfma16x16x32(k1, qf[c][1], s[c][t4]);
       }
     }
-    // mask keys beyond T, scale to log2 domain, tile max
-    const int key0 = kt * KT + hq * 4;
-    float mx = -INFINITY;
+    if (kt * KT + KT > T) {  // last, partial tile: keys >= T -> -inf
+      const int key0 = kt * KT + hq * 4;
 #pragma unroll
-    for (int t4 = 0; t4 < 4; ++t4)
+      for (int c = 0; c < NQ; ++c)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const int key = key0 + t4 * 16 + r;
-        const float z = key < T ? s[t4][r] * LOG2E : -INFINITY;
-        s[t4][r] = z;
-        mx = fmaxf(mx, z);
+        for (int t4 = 0; t4 < 4; ++t4)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (key0 + t4 * 16 + r >= T) s[c][t4][r] = -INFINITY;
+    }
+    f16x8 pb[NQ][2];
+#pragma unroll
+    for (int c = 0; c < NQ; ++c) {
+      float mx = fmaxf(fmaxf(fmaxf(s[c][0][0], s[c][0][1]), fmaxf(s[c][0][2], s[c][0][3])),
+                       fmaxf(fmaxf(s[c][1][0], s[c][1][1]), fmaxf(s[c][1][2], s[c][1][3])));
+      mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(s[c][2][0], s[c][2][1]), fmaxf(s[c][2][2], s[c][2][3])),
+                           fmaxf(fmaxf(s[c][3][0], s[c][3][1]), fmaxf(s[c][3][2], s[c][3][3]))));
+      mx = xmax4(mx);  // max of S' over the tile (relative to m_run)
+      if (FIRST || __any(mx > 0.f)) {
+        // the running max grows by delta >= 0: shift S', rescale O and l
+        const float delta = FIRST ? mx : fmaxf(mx, 0.f);
+        m_run[c] += delta;
+        negm[c] = f32x4{-m_run[c], -m_run[c], -m_run[c], -m_run[c]};
+#pragma unroll
+        for (int t4 = 0; t4 < 4; ++t4) s[c][t4] -= delta;
+        if (!FIRST) {
+          const float alpha = __builtin_amdgcn_exp2f(-delta);
+          l_run[c] *= alpha;
+#pragma unroll
+          for (int d = 0; d < 4; ++d) acc[c][d] *= alpha;
+        }
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-    const float m_new = fmaxf(m_run, mx);
-    const float alpha = exp2f(m_run - m_new);
-    m_run = m_new;
-    float ls = 0.f;
+      float ls = 0.f;
 #pragma unroll
-    for (int t4 = 0; t4 < 4; ++t4)
+      for (int t4 = 0; t4 < 4; ++t4)
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        const float pv = exp2f(s[t4][r] - m_new);
-        s[t4][r] = pv;
-        ls += pv;
-      }
-    l_run = l_run * alpha + ls;
+        for (int r = 0; r < 4; ++r) {
+          const float pv = __builtin_amdgcn_exp2f(s[c][t4][r]);
+          s[c][t4][r] = pv;
+          ls += pv;
+        }
+      l_run[c] += ls;
+      // P^T as B operand: k index j<4 -> key sub-tile 2ks, j>=4 -> 2ks+1 (rows 4hq+r)
 #pragma unroll
-    for (int d = 0; d < 4; ++d) acc[d] *= alpha;
-
-    // P^T as B operand: k-index j<4 -> key sub-tile 2ks, j>=4 -> 2ks+1 (rows 4hq+r)
-    f16x8 pb[2];
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        pb[ks][r] = (f16)s[2 * ks][r];
-        pb[ks][4 + r] = (f16)s[2 * ks + 1][r];
-      }
-    // O^T[dh][q] += V^T[dh][key] P^T[key][q]
+        for (int r = 0; r < 4; ++r) {
+          pb[c][ks][r] = (f16)s[c][2 * ks][r];
+          pb[c][ks][4 + r] = (f16)s[c][2 * ks + 1][r];
+        }
+    }
+    // O^T[dh][q] += V^T[dh][key] P^T[key][q]; V^T keys are stored vt_pos-
+    // permuted, so the 8 keys of k-step ks for lane slot hq are one 16-B chunk
 #pragma unroll
     for (int d = 0; d < 4; ++d) {
       const int row = d * 16 + l15;
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        const int ka = 32 * ks + 4 * hq;  // keys ka..ka+3 and ka+16..ka+19
-        const int kb2 = ka + 16;
-        const f16x4v lo = *reinterpret_cast<const f16x4v*>(V_ + vswz(row, ka >> 3) + (ka & 7));
-        const f16x4v hi = *reinterpret_cast<const f16x4v*>(V_ + vswz(row, kb2 >> 3) + (kb2 & 7));
-        f16x8 af;
+        const f16x8 af = *reinterpret_cast<const f16x8*>(V_ + kswz(row, 4 * ks + hq));
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          af[r] = lo[r];
-          af[4 + r] = hi[r];
-        }
-        acc[d] = mfma16x16x32(af, pb[ks], acc[d]);
+        for (int c = 0; c < NQ; ++c) acc[c][d] = mfma16x16x32(af, pb[c][ks], acc[c][d]);
       }
     }
-    if (kt + 1 < nkt) stash(cur ^ 1);
-    __syncthreads();
+  };
+
+  int slot = 0;
+  for (int kt = 0; kt < nkt; ++kt) {
+    if (kt + 2 < nkt) issue(kt + 2, slot == 0 ? 2 : slot - 1);
+    if (kt == 0) tile(kt, slot, std::true_type{});
+    else tile(kt, slot, std::false_type{});
+    // tile kt+1 must have landed before anyone reads it; its slot's previous
+    // contents (tile kt-2) were released at the previous barrier
+    if (kt + 2 < nkt) wait_vm_n<PER_TILE>();
+    else wait_vm_n<0>();
+    lds_barrier();
+    slot = slot == 2 ? 0 : slot + 1;
   }
 
-  float lt = l_run;
-  lt += __shfl_xor(lt, 16, 64);
-  lt += __shfl_xor(lt, 32, 64);
-  const float inv = 1.f / lt;
-  const int qi = qbase + l15;
-  if (qi < T) {
-    f16* orow = o + ((size_t)b * T + qi) * ldo + h * 64;
 #pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      f16x4v v;
+  for (int c = 0; c < NQ; ++c) {
+    const float lt = xsum4(l_run[c]);
+    const float inv = 1.f / lt;
+    const int qi = qbase + c * 16 + l15;
+    if (qi < T) {
+      f16* orow = o + ((size_t)b * T + qi) * ldo + h * 64;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = (f16)(acc[d][r] * inv);
-      *reinterpret_cast<f16x4v*>(orow + d * 16 + hq * 4) = v;
+      for (int d = 0; d < 4; ++d) {
+        f16x4v v;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = (f16)(acc[c][d][r] * inv);
+        *reinterpret_cast<f16x4v*>(orow + d * 16 + hq * 4) = v;
+      }
     }
   }
 }
 
+template <int QW, int NW>
+hipError_t run_attn(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T, int Tpad, int ldo,
+                    hipStream_t st) {
+  constexpr int BQ = QW * NW;
+  dim3 grid((T + BQ - 1) / BQ, B * H);
+  hipLaunchKernelGGL((attn_fwd_kernel<QW, NW>), grid, dim3(NW * 64), 0, st, reinterpret_cast<const f16*>(q),
+                     reinterpret_cast<const f16*>(k), reinterpret_cast<const f16*>(vt), reinterpret_cast<f16*>(o), H,
+                     T, Tpad, ldo);
+  return hipGetLastError();
+}
+
 }  // namespace
 
-hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T,
-                            int Tpad, int ldo, hipStream_t st) {
+hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T, int Tpad,
+                            int ldo, hipStream_t st) {
   if (B <= 0 || T <= 0) return hipSuccess;
-  if (Tpad % KT || Tpad < ((T + KT - 1) / KT) * KT) return hipErrorInvalidValue;
-  dim3 grid((T + 63) / 64, B * H);
-  hipLaunchKernelGGL(attn_fwd_kernel, grid, dim3(256), 0, st, reinterpret_cast<const f16*>(q),
-                     reinterpret_cast<const f16*>(k), reinterpret_cast<const f16*>(vt),
-                     reinterpret_cast<f16*>(o), H, T, Tpad, ldo);
-  return hipGetLastError();
+  if (Tpad % KT || Tpad < ((T + KT - 1) / KT) * KT || (ldo & 3)) return hipErrorInvalidValue;
+  // tuning override: MDE_ATTN_CFG = 32x4 | 16x8 | 16x4 | 16x2 (queries/wave x waves)
+  static const int forced = [] {
+    const char* e = getenv("MDE_ATTN_CFG");
+    if (!e) return 0;
+    if (!strcmp(e, "32x4")) return 1;
+    if (!strcmp(e, "16x8")) return 2;
+    if (!strcmp(e, "16x4")) return 3;
+    if (!strcmp(e, "16x2")) return 4;
+    return 0;
+  }();
+  switch (forced) {
+    case 1: return run_attn<32, 4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
+    case 2: return run_attn<16, 8>(q, k, vt, o, B, H, T, Tpad, ldo, st);
+    case 3: return run_attn<16, 4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
+    case 4: return run_attn<16, 2>(q, k, vt, o, B, H, T, Tpad, ldo, st);
+    default: break;
+  }
+  // measured on MI355X (tools/bench_kernels.py, T 1370, H 6): 128-query
+  // workgroups of 8 waves win once they fill the chip (B 32: 181 us vs 230 us
+  // for 64-query groups); at B 1 the 64-query groups fill more CUs (21 vs 23 us)
+  const long long g128 = (long long)((T + 127) / 128) * B * H;
+  if (g128 >= 256) return run_attn<16, 8>(q, k, vt, o, B, H, T, Tpad, ldo, st);
+  return run_attn<16, 4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
 }
 
 }  // namespace mde

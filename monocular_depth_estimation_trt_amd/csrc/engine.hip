@@ -401,7 +401,7 @@ struct Runner {
         g.T = T;
         g.Tpad = e.Tpad;
         g.heads = e.H;
-        g.qscale = 0.125f;  // dh^-0.5, dh = 64 (exact in f16)
+        g.qscale = 0.125f * 1.4426950408889634f;  // dh^-0.5 * log2(e): scores in log2 units
         snprintf(nm, sizeof nm, "block%d.qkv", i);
         gemm(nm, g);
       }

@@ -38,6 +38,15 @@ MDE_DEV float erf_fast(float x) {
 // GELU with the exact-erf definition (nn.GELU() default, upstream DINOv2 Mlp).
 MDE_DEV float gelu_erf(float x) { return 0.5f * x * (1.0f + erf_fast(x * 0.70710678118654752f)); }
 
+// Storage position of key t in a V^T row: inside every 32-key group the keys
+// are ordered [4 keys of sub-tile 0 | 4 keys of sub-tile 1] per 4-key lane
+// slot, so the 8 keys one MFMA lane consumes in P.V ({32g+4h+0..3,
+// 32g+16+4h+0..3}) are one contiguous 16-byte read.
+MDE_DEV int vt_pos(int t) {
+  const int k = t & 31;
+  return (t & ~31) | ((k & 15) >> 2) << 3 | (k >> 4) << 2 | (k & 3);
+}
+
 MDE_DEV f16x8 zero8() {
   f16x8 z;
 #pragma unroll

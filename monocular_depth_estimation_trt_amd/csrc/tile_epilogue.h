@@ -80,7 +80,7 @@ MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&m
           const int b = m / p.T, t = m - (m / p.T) * p.T;
           const size_t bh = (size_t)b * p.heads + (w >> 6);
           if (which == 2) {
-            f16* dst = reinterpret_cast<f16*>(p.vt) + (bh * 64 + (w & 63)) * p.Tpad + t;
+            f16* dst = reinterpret_cast<f16*>(p.vt) + (bh * 64 + (w & 63)) * p.Tpad + vt_pos(t);
 #pragma unroll
             for (int r = 0; r < 4; ++r) dst[(size_t)r * p.Tpad] = (f16)v[r];
           } else {

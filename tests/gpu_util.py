@@ -35,6 +35,17 @@ def op(name: str, *args) -> None:
         _KEEP.clear()
 
 
+def vt_pos(t):
+    """Key permutation of the V^T layout (csrc/mde_device.h vt_pos)."""
+    k = t & 31
+    return (t & ~31) | (((k & 15) >> 2) << 3) | ((k >> 4) << 2) | (k & 3)
+
+
+def vt_perm(T: int) -> torch.Tensor:
+    """Index tensor: storage column of key t, t in [0, T)."""
+    return torch.tensor([vt_pos(t) for t in range(T)], dtype=torch.long)
+
+
 def pad_w(w: torch.Tensor, n_mult: int = 128, k_mult: int = 64) -> torch.Tensor:
     """[N][K] -> f16 [Npad][Kpad] zero-padded device tensor (the packer's layout)."""
     n, k = w.shape

@@ -14,7 +14,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from gpu_util import close, conv_w, nchw, nhwc, op, pad_w, ptr, stream
+from gpu_util import close, conv_w, nchw, nhwc, op, pad_w, ptr, stream, vt_perm
 
 pytestmark = pytest.mark.gpu
 
@@ -77,25 +77,37 @@ def test_qkv_layout(gpu):
     rv = full[:, :, 2].permute(0, 2, 3, 1).reshape(B * H, 64, T)
     close(q[:, :T], rq, 1e-2, 1e-2, "q")
     close(k[:, :T], rk, 1e-2, 1e-2, "k")
-    close(vt[:, :, :T], rv, 1e-2, 1e-2, "vt")
-    assert float(q[:, T:].abs().max()) == 0 and float(vt[:, :, T:].abs().max()) == 0, "pad must stay zero"
+    perm = vt_perm(T).to(gpu)
+    close(vt[:, :, perm], rv, 1e-2, 1e-2, "vt (key-permuted storage)")
+    pad = torch.ones(Tp, dtype=torch.bool, device=gpu)
+    pad[perm] = False
+    assert float(q[:, T:].abs().max()) == 0 and float(vt[:, :, pad].abs().max()) == 0, "pad must stay zero"
 
 
-@pytest.mark.parametrize("B,H,T", [(2, 6, 50), (1, 6, 1370), (1, 2, 64), (3, 1, 65), (1, 16, 130)])
+LOG2E = 1.4426950408889634
+
+
+def attn_ref(q, k, v):
+    """q is pre-scaled by dh^-0.5 * log2(e) (the kernel's contract): scores are
+    in log2 units, softmax base 2 == softmax base e of scores * ln 2."""
+    qh, kh, vh = q.half().float(), k.half().float(), v.half().float()
+    return torch.softmax((qh @ kh.transpose(1, 2)) / LOG2E, dim=-1) @ vh
+
+
+@pytest.mark.parametrize("B,H,T", [(2, 6, 50), (1, 6, 1370), (1, 2, 64), (3, 1, 65), (1, 16, 130),
+                                   (32, 6, 200), (8, 6, 1370), (1, 1, 1)])
 def test_attention(gpu, B, H, T):
     Tp = -(-T // 64) * 64
-    q = rn(B * H, T, 64) * 0.125 * 2.0
+    q = rn(B * H, T, 64) * 0.125 * 2.0 * LOG2E
     k = rn(B * H, T, 64) * 2.0
     v = rn(B * H, T, 64)
-    qh, kh, vh = q.half().float(), k.half().float(), v.half().float()
-    p = torch.softmax(qh @ kh.transpose(1, 2), dim=-1)
-    ref = (p @ vh).reshape(B, H, T, 64).permute(0, 2, 1, 3).reshape(B * T, H * 64)
+    ref = attn_ref(q, k, v).reshape(B, H, T, 64).permute(0, 2, 1, 3).reshape(B * T, H * 64)
     qg = torch.zeros(B * H, Tp, 64, dtype=torch.float16, device=gpu)
     kg = torch.zeros_like(qg)
     vtg = torch.zeros(B * H, 64, Tp, dtype=torch.float16, device=gpu)
     qg[:, :T] = q.half().to(gpu)
     kg[:, :T] = k.half().to(gpu)
-    vtg[:, :, :T] = v.transpose(1, 2).half().to(gpu)
+    vtg[:, :, vt_perm(T).to(gpu)] = v.transpose(1, 2).half().to(gpu)
     o = torch.empty(B * T, H * 64, dtype=torch.float16, device=gpu)
     op("mde_op_attention", ptr(qg), ptr(kg), ptr(vtg), ptr(o), B, H, T, Tp, H * 64, stream())
     close(o, ref, 2e-2, 5e-3, f"attention B{B} H{H} T{T}")
@@ -110,13 +122,13 @@ def test_attention_spiky_rows(gpu):
     k[:, 290] = q[:, :].mean(1) * 60.0                 # huge score for key 290 (last tile)
     k[:, 5] = q[:, :].mean(1) * 30.0                   # large early key
     v = rn(B * H, T, 64)
-    qh, kh, vh = q.half().float(), k.half().float(), v.half().float()
-    ref = (torch.softmax(qh @ kh.transpose(1, 2), -1) @ vh).reshape(B, H, T, 64).permute(0, 2, 1, 3)
+    ref = attn_ref(q, k, v).reshape(B, H, T, 64).permute(0, 2, 1, 3)
     ref = ref.reshape(B * T, H * 64)
     qg = torch.zeros(B * H, Tp, 64, dtype=torch.float16, device=gpu)
     kg = torch.zeros_like(qg)
     vtg = torch.zeros(B * H, 64, Tp, dtype=torch.float16, device=gpu)
-    qg[:, :T], kg[:, :T], vtg[:, :, :T] = q.half().to(gpu), k.half().to(gpu), v.transpose(1, 2).half().to(gpu)
+    qg[:, :T], kg[:, :T] = q.half().to(gpu), k.half().to(gpu)
+    vtg[:, :, vt_perm(T).to(gpu)] = v.transpose(1, 2).half().to(gpu)
     o = torch.empty(B * T, H * 64, dtype=torch.float16, device=gpu)
     op("mde_op_attention", ptr(qg), ptr(kg), ptr(vtg), ptr(o), B, H, T, Tp, H * 64, stream())
     close(o, ref, 2e-2, 5e-3, "attention spiky")
