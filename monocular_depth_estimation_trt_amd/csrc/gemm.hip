@@ -37,6 +37,9 @@
 #ifndef MDE_GEMM_BK
 #define MDE_GEMM_BK 64
 #endif
+#ifndef MDE_XCD_REMAP
+#define MDE_XCD_REMAP 1
+#endif
 
 namespace mde {
 
@@ -85,7 +88,16 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
   const int ntn = (p.N + BN - 1) / BN;
-  const int tm = blockIdx.x / ntn, tn = blockIdx.x - tm * ntn;
+  // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs
+  // (bid % 8 shares an L2), so give each XCD a contiguous run of tiles
+  // (tn fastest) -- the N-tiles of one row block then share A in one L2.
+  // Bijective for any grid size (cdna_hip_programming.md section 5).
+  int bid = blockIdx.x;
+  if (MDE_XCD_REMAP) {
+    const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
+    bid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  }
+  const int tm = bid / ntn, tn = bid - tm * ntn;
   const int m0 = tm * BM, n0 = tn * BN;
 
   // ---- glds lane geometry: lane -> (row within a wave-instruction, chunk)
@@ -327,6 +339,11 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
   if (p.emode == E_CONVT && (p.cout & 7)) return hipErrorInvalidValue;
   if (p.emode == E_HEAD && (p.N != 32 || p.amode == A_DENSE)) return hipErrorInvalidValue;
   if (p.amode != A_DENSE && conv_direct_supported(p) && !getenv_im2col()) return launch_conv3(p, st);
+  if (p.amode == A_DENSE && gemm_persistent_enabled()) {
+    // one 256x128 tile per CU per round at least: the persistent pipeline wins
+    const long long tiles = (long long)((p.M + 255) / 256) * ((p.N + 127) / 128);
+    if (tiles >= 256) return launch_gemm_persistent(p, st);
+  }
   switch (p.amode) {
     case A_DENSE:
       switch (p.emode) {

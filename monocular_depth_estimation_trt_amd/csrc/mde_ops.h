@@ -60,6 +60,11 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st);
 bool conv_direct_supported(const GemmParams& p);
 hipError_t launch_conv3(const GemmParams& p, hipStream_t st);
 
+// Persistent pipelined dense GEMM (gemm_persistent.hip); launch_gemm routes
+// large dense problems here when MDE_GEMM_PERSISTENT=1 (A/B tuning path).
+bool gemm_persistent_enabled();
+hipError_t launch_gemm_persistent(const GemmParams& p, hipStream_t st);
+
 hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T,
                             int Tpad, int ldo, hipStream_t st);
 

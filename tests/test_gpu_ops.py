@@ -30,7 +30,9 @@ def f16(t, dev):
 
 
 @pytest.mark.parametrize("m,n,k,act", [(300, 200, 96, 0), (1370, 1152, 384, 0), (777, 1536, 384, 2),
-                                       (64, 48, 48, 1), (5, 32, 64, 1), (2048, 384, 1536, 0)])
+                                       (64, 48, 48, 1), (5, 32, 64, 1), (2048, 384, 1536, 0),
+                                       # >= 256 tiles of 256x128: the persistent pipelined kernel
+                                       (16384, 1536, 384, 2), (33000, 1024, 200, 1), (65537, 512, 64, 0)])
 def test_linear(gpu, m, n, k, act):
     a, w, b = rn(m, k), rn(n, k, scale=k ** -0.5), rn(n, scale=0.1)
     a16, w16 = a.half().float(), w.half().float()
@@ -46,8 +48,8 @@ def test_linear(gpu, m, n, k, act):
     close(out, ref, 1e-2, 1e-2, f"linear {m}x{n}x{k} act{act}")
 
 
-def test_linear_residual(gpu):
-    m, n, k = 1370, 384, 1536
+@pytest.mark.parametrize("m,n,k", [(1370, 384, 1536), (43840, 384, 1536)])
+def test_linear_residual(gpu, m, n, k):
     a, w, b = rn(m, k), rn(n, k, scale=k ** -0.5), rn(n, scale=0.1)
     ls = 0.5 + 0.05 * rn(n)
     x = rn(m, n)
@@ -59,10 +61,10 @@ def test_linear_residual(gpu):
     close(xg, ref, 2e-3, 2e-3, "linear_residual")
 
 
-def test_qkv_layout(gpu):
-    B, T, H = 2, 50, 6
+@pytest.mark.parametrize("B,T,H", [(2, 50, 6), (16, 1370, 6)])
+def test_qkv_layout(gpu, B, T, H):
     D = 64 * H
-    Tp = 64
+    Tp = -(-T // 64) * 64
     a, w, b = rn(B * T, D), rn(3 * D, D, scale=D ** -0.5), rn(3 * D, scale=0.1)
     full = a.half().float() @ w.half().float().T + b                         # [B*T, 3D]
     full = full.reshape(B, T, 3, H, 64)
@@ -148,7 +150,7 @@ def test_layernorm(gpu, D, skip):
     close(y, ref, 1e-2, 1e-2, f"layernorm D{D} skip{skip}")
 
 
-@pytest.mark.parametrize("B,Hh,Ww", [(2, 98, 98), (1, 126, 182)])
+@pytest.mark.parametrize("B,Hh,Ww", [(2, 98, 98), (1, 126, 182), (16, 518, 518)])
 def test_patch_embed(gpu, B, Hh, Ww):
     D = 384
     ph, pw = Hh // 14, Ww // 14
@@ -204,9 +206,9 @@ def test_conv3x3_up(gpu, B, sh, sw, uh, uw, cin, cout):
     close(nchw(out), ref, 1e-2, 1.5e-2, "conv3x3_up")
 
 
-@pytest.mark.parametrize("s,cin", [(4, 48), (2, 96), (4, 256)])
-def test_conv_transpose(gpu, s, cin):
-    B, h, w = 2, 7, 9
+@pytest.mark.parametrize("s,cin,B,h,w", [(4, 48, 2, 7, 9), (2, 96, 2, 7, 9), (4, 256, 2, 7, 9),
+                                        (4, 48, 32, 37, 37), (2, 512, 8, 37, 37)])
+def test_conv_transpose(gpu, s, cin, B, h, w):
     cout = cin
     x = rn(B, cin, h, w)
     wt, b = rn(cin, cout, s, s, scale=cin ** -0.5), rn(cout, scale=0.02)
