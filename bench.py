@@ -197,26 +197,13 @@ def main():
     st = torch.cuda.Stream()
     sh = st.cuda_stream
 
-    def barrier():
-        if dist is not None:
-            dist.barrier()
-
+    from monocular_depth_estimation_trt_amd import replicas
     for _ in range(a.warmup):
         ctx.execute_async_v3(sh)
     torch.cuda.synchronize()
-    barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(a.steps):
-        ctx.execute_async_v3(sh)
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    barrier()
-    el = t1 - t0
-    if dist is not None:
-        t = torch.tensor([el], dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
+    el = replicas.timed_region(lambda: ctx.execute_async_v3(sh), a.steps, torch.cuda.synchronize,
+                               dist.barrier if dist is not None else None)
+    el = replicas.max_over_ranks(el)
     out_ok = bool(torch.isfinite(y).all().item())
     value = world * B * a.steps / el
     ms_step = el / a.steps * 1e3

@@ -1,0 +1,72 @@
+"""Depth Anything V2 on MI355X -- the counterpart of the reference driver
+`models/depth_anything_v2/onnx2trt.py:main` (:42-127), same sequence:
+
+  input -> get_engine -> create_execution_context -> allocate_buffers ->
+  bench.measure(do_inference) (20 warmup / 100 iterations) ->
+  post-process (bilinear align_corners=True back to the source size, clamp
+  [1e-3, 1e3], outside the timed loop) -> bench.record
+
+    python -m monocular_depth_estimation_trt_amd.models.depth_anything_v2.run \
+        [--source synthetic:vits:metric | ckpt.pth] [--input x.npy] [--src-hw H W]
+
+`--input` is an already-preprocessed float32 NCHW [1,3,518,518] tensor (the
+reference's core/preprocess.py needs cv2, absent here); without it a
+synthetic image of the spec's input domain is used.
+"""
+
+import argparse
+import os
+
+import numpy as np
+
+from monocular_depth_estimation_trt_amd import bench, common, spec, weights
+from monocular_depth_estimation_trt_amd.common_runtime import allocate_buffers, do_inference, free_buffers
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+
+
+def postprocess(depth: np.ndarray, src_hw) -> np.ndarray:
+    """onnx2trt.py:111-117: bilinear(align_corners=True) to the source size, clamp."""
+    import torch
+    import torch.nn.functional as F
+    t = torch.from_numpy(np.ascontiguousarray(depth))[:, None]
+    t = F.interpolate(t, tuple(src_hw), mode="bilinear", align_corners=True)[0, 0]
+    return torch.clamp(t, min=1e-3, max=1e3).numpy()
+
+
+def main(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--source", default="synthetic:vits:metric:1234")
+    ap.add_argument("--engine", default=os.path.join(HERE, "engine", "depth_anything_v2_vits_518x518_fp16.mdeng"))
+    ap.add_argument("--input", default="")
+    ap.add_argument("--src-hw", type=int, nargs=2, default=[2268, 3024])
+    ap.add_argument("--iterations", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--out-dir", default=os.path.join(os.getcwd(), "reports", "bench"))
+    a = ap.parse_args(argv)
+
+    s = spec.load("depth_anything_v2")
+    mc = spec.model_config_of(s)
+    input_h, input_w = mc["input_hw"]
+    x = (np.load(a.input, allow_pickle=False).astype(np.float32) if a.input
+         else weights.synthetic_images(1, input_h, input_w, first_seed=0))
+    output_shape = (1, input_h, input_w)
+    with common.get_engine(a.source, a.engine, "fp16", None, encoder=mc["encoder"], depth_type=mc["depth_type"],
+                           max_depth=mc["max_depth"], input_hw=(input_h, input_w)) as engine, \
+            engine.create_execution_context() as context:
+        inputs, outputs, bindings, stream = allocate_buffers(engine, output_shape, profile_idx=0)
+        inputs[0].host = x
+        outs, samples = bench.measure(
+            lambda: do_inference(context, engine=engine, bindings=bindings, inputs=inputs, outputs=outputs,
+                                 stream=stream), warmup=a.warmup, iterations=a.iterations)
+        depth = postprocess(outs[0].reshape(output_shape), a.src_hw)
+        bench.record("depth_anything_v2", samples, warmup=a.warmup, precision="fp16", profile="bench",
+                     input_h=input_h, input_w=input_w, engine_path=a.engine, outputs={"depth": depth},
+                     encoder=mc["encoder"], notes=f"source={a.source}", model_input=x, out_dir=a.out_dir)
+        print(f"[MDET] max : {depth.max():0.5f} , min : {depth.min():0.5f}")
+        free_buffers(inputs, outputs, stream)
+    return depth
+
+
+if __name__ == "__main__":
+    main()
