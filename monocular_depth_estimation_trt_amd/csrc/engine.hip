@@ -63,6 +63,7 @@ struct mde_engine {
   // derived geometry
   int ph = 0, pw = 0, np = 0, T = 0, Tpad = 0, D = 0, H = 0, F = 0;
   int h4 = 0, w4 = 0;
+  int c1p = 0;          // reassemble-0 channels padded to a multiple of 32 (direct-conv input)
   float head_b2 = 0.f;  // output_conv2.2 bias (scalar kernel argument)
 
   const DevTensor* get(const std::string& n) const {
@@ -78,6 +79,7 @@ struct Buf {
   float* X;
   h16 *tap[4], *pj[4], *l1, *l2, *l4, *rn[4];
   h16 *tb, *sb, *ub, *vb, *p4, *p3, *p2, *c1;
+  unsigned* lncnt;  // fused-LayerNorm row-block arrival counters (zeroed, self-resetting)
 };
 
 struct GraphKey {
@@ -174,6 +176,7 @@ int load_pack(const uint8_t* data, size_t n, int device, mde_engine** out) {
   e->Tpad = (e->T + 63) / 64 * 64;
   e->h4 = (e->ph + 1) / 2;
   e->w4 = (e->pw + 1) / 2;
+  e->c1p = (c.out_channels[0] + 31) / 32 * 32;
   // every tensor the forward uses must be present
   std::vector<std::string> need = {"patch.w", "patch.b", "pos.patch", "pos.cls", "norm.g", "norm.b",
                                    "rs0.w", "rs0.b", "rs1.w", "rs1.b", "rs3.w", "rs3.b",
@@ -233,7 +236,7 @@ size_t plan_arena(const mde_engine& e, int B, Buf* b, uint8_t* base) {
   t.Mh = (h16*)take(bb * e.T * e.cfg.mlp_hidden * 2);
   for (int i = 0; i < 4; ++i) t.tap[i] = (h16*)take(bb * np * D * 2);
   for (int i = 0; i < 4; ++i) t.pj[i] = (h16*)take(bb * np * oc[i] * 2);
-  t.l1 = (h16*)take(bb * s1 * oc[0] * 2);
+  t.l1 = (h16*)take(bb * s1 * e.c1p * 2);  // channels padded to a multiple of 32 (pad stays 0)
   t.l2 = (h16*)take(bb * s2 * oc[1] * 2);
   t.l4 = (h16*)take(bb * s4 * oc[3] * 2);
   const size_t ss[4] = {s1, s2, s3, s4};
@@ -246,8 +249,22 @@ size_t plan_arena(const mde_engine& e, int B, Buf* b, uint8_t* base) {
   t.p3 = (h16*)take(bb * s2 * F * 2);
   t.p2 = (h16*)take(bb * s1 * F * 2);
   t.c1 = (h16*)take(bb * s0 * (F / 2) * 2);
+  t.lncnt = (unsigned*)take((bb * e.T / 32 + 1) * 4);  // >= one word per 32-row block
   if (b) *b = t;
   return off;
+}
+
+// MDE_FUSE_LN=1 folds the LayerNorms into the proj/fc2 epilogues (row-block
+// arrival counter + agent-scope release/acquire).  Opt-in: measured slower
+// on MI355X (r01: proj 54 -> 113 us, fc2 98 -> 156 us at B=32) because every
+// agent-scope release/acquire writes back / invalidates the XCD's whole L2,
+// evicting the operand tiles of the other workgroups on that XCD.
+static bool fuse_ln_enabled() {
+  static const int v = [] {
+    const char* e = getenv("MDE_FUSE_LN");
+    return (e && e[0] == '1') ? 1 : 0;
+  }();
+  return v != 0;
 }
 
 // ---- the forward schedule ----------------------------------------------------
@@ -385,12 +402,35 @@ struct Runner {
     }
     int tap = 0;
     char nm[64];
+    const bool fuse = fuse_ln_enabled() && (D == 384 || D == 768 || D == 1024);
+    // fused LayerNorm in a residual GEMM's tail: out1 = LN(g1,b1) (token
+    // layout), out2 = final norm into a tap map (cls dropped)
+    auto fuse_ln = [&](GemmParams& g, const char* g1, const char* b1, h16* tapdst) {
+      if (!fuse) return;
+      g.ln_counter = b.lncnt;
+      g.ln_eps = cf.ln_eps;
+      g.ln_T = T;
+      if (g1) {
+        g.ln1_g = w32(g1);
+        g.ln1_b = w32(b1);
+        g.ln1_out = b.Hn;
+      }
+      if (tapdst) {
+        g.ln2_g = w32("norm.g");
+        g.ln2_b = w32("norm.b");
+        g.ln2_out = tapdst;
+        g.ln2_skip = 1;
+      }
+    };
     for (int i = 0; i < cf.depth; ++i) {
       const std::string p = "b" + std::to_string(i) + ".";
-      snprintf(nm, sizeof nm, "block%d.norm1", i);
-      step(nm, [&] {
-        return launch_layernorm(b.X, b.Hn, w32(p + "ln1.g"), w32(p + "ln1.b"), B * T, D, cf.ln_eps, T, 0, st);
-      });
+      const std::string pn = "b" + std::to_string(i + 1) + ".";
+      if (!fuse || i == 0) {
+        snprintf(nm, sizeof nm, "block%d.norm1", i);
+        step(nm, [&] {
+          return launch_layernorm(b.X, b.Hn, w32(p + "ln1.g"), w32(p + "ln1.b"), B * T, D, cf.ln_eps, T, 0, st);
+        });
+      }
       {
         GemmParams g = dense(b.Hn, D, p + "qkv.w", B * T, 3 * D, D);
         g.emode = E_QKV;
@@ -414,13 +454,17 @@ struct Runner {
         g.ls = w32(p + "ls1");
         g.x32 = b.X;
         g.ldo = D;
+        const std::string lg = p + "ln2.g", lb = p + "ln2.b";
+        fuse_ln(g, lg.c_str(), lb.c_str(), nullptr);
         snprintf(nm, sizeof nm, "block%d.proj", i);
         gemm(nm, g);
       }
-      snprintf(nm, sizeof nm, "block%d.norm2", i);
-      step(nm, [&] {
-        return launch_layernorm(b.X, b.Hn, w32(p + "ln2.g"), w32(p + "ln2.b"), B * T, D, cf.ln_eps, T, 0, st);
-      });
+      if (!fuse) {
+        snprintf(nm, sizeof nm, "block%d.norm2", i);
+        step(nm, [&] {
+          return launch_layernorm(b.X, b.Hn, w32(p + "ln2.g"), w32(p + "ln2.b"), B * T, D, cf.ln_eps, T, 0, st);
+        });
+      }
       {
         GemmParams g = dense(b.Hn, D, p + "fc1.w", B * T, cf.mlp_hidden, D);
         g.emode = E_STORE;
@@ -438,10 +482,15 @@ struct Runner {
         g.ls = w32(p + "ls2");
         g.x32 = b.X;
         g.ldo = D;
+        const bool tapped = tap < 4 && cf.taps[tap] == i;
+        const std::string lg = pn + "ln1.g", lb = pn + "ln1.b";
+        fuse_ln(g, i + 1 < cf.depth ? lg.c_str() : nullptr, lb.c_str(), tapped ? b.tap[tap] : nullptr);
         snprintf(nm, sizeof nm, "block%d.fc2", i);
         gemm(nm, g);
       }
-      if (tap < 4 && cf.taps[tap] == i) {
+      if (fuse && tap < 4 && cf.taps[tap] == i) {
+        ++tap;
+      } else if (tap < 4 && cf.taps[tap] == i) {
         snprintf(nm, sizeof nm, "tap%d.norm", tap);
         h16* dst = b.tap[tap];
         step(nm, [&] {
@@ -469,6 +518,7 @@ struct Runner {
       g.out16 = b.l1;
       g.s = 4;
       g.cout = oc[0];
+      g.ldo = e.c1p;
       g.ih = e.ph;
       g.iw = e.pw;
       gemm("reassemble0.convT4", g);
@@ -480,6 +530,7 @@ struct Runner {
       g.out16 = b.l2;
       g.s = 2;
       g.cout = oc[1];
+      g.ldo = oc[1];
       g.ih = e.ph;
       g.iw = e.pw;
       gemm("reassemble1.convT2", g);
@@ -493,8 +544,9 @@ struct Runner {
     const int hs[4] = {4 * e.ph, 2 * e.ph, e.ph, e.h4};
     const int ws[4] = {4 * e.pw, 2 * e.pw, e.pw, e.w4};
     const h16* lay[4] = {b.l1, b.l2, b.pj[2], b.l4};
+    const int cin[4] = {e.c1p, oc[1], oc[2], oc[3]};
     for (int i = 0; i < 4; ++i) {
-      GemmParams g = conv(lay[i], B, hs[i], ws[i], oc[i], "rn" + std::to_string(i + 1) + ".w", F, 1);
+      GemmParams g = conv(lay[i], B, hs[i], ws[i], cin[i], "rn" + std::to_string(i + 1) + ".w", F, 1);
       g.out16 = b.rn[i];
       snprintf(nm, sizeof nm, "layer%d_rn", i + 1);
       gemm(nm, g);
@@ -1123,6 +1175,7 @@ int mde_op_conv_transpose(const void* in, int batch, int h, int w, int cin, cons
   g.out16 = (h16*)out;
   g.s = stride;
   g.cout = cout;
+  g.ldo = cout;
   g.ih = h;
   g.iw = w;
   OP_RET(launch_gemm(g, (hipStream_t)st), "conv_transpose");

@@ -51,6 +51,13 @@ struct GemmParams {
   // E_HEAD
   const float* w2 = nullptr; float b2 = 0.f; int head_metric = 1; float max_depth = 1.f;
   float* out32 = nullptr;
+  // E_RESID + fused LayerNorm of the finished rows (ln_counter != null): the
+  // last workgroup of each row block normalises rows [m0, m0+BM) of x32 into
+  // up to two f16 outputs (gamma/beta each; skip_cls -> tap token-map layout)
+  unsigned* ln_counter = nullptr;  // one zeroed word per row block, self-resetting
+  float ln_eps = 1e-6f; int ln_T = 1;
+  const float *ln1_g = nullptr, *ln1_b = nullptr; h16* ln1_out = nullptr; int ln1_skip = 0;
+  const float *ln2_g = nullptr, *ln2_b = nullptr; h16* ln2_out = nullptr; int ln2_skip = 0;
 };
 
 hipError_t launch_gemm(const GemmParams& p, hipStream_t st);

@@ -13,7 +13,7 @@ namespace mde {
 
 template <int EM, int TM, int TN>
 MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&mrow)[TM], int ncol, int lane) {
-    if constexpr (EM == E_HEAD) {
+  if constexpr (EM == E_HEAD) {
     static_assert(TN == 2, "head epilogue needs the full 32-channel row in one wave (BN 32, WN 1)");
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
@@ -113,7 +113,7 @@ MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&m
           const int b = m / hw, rem = m - (m / hw) * hw;
           const int y = rem / p.iw, x = rem - (rem / p.iw) * p.iw;
           const int OH = p.ih * p.s, OW = p.iw * p.s;
-          const size_t o = (((size_t)b * OH + y * p.s + dy) * OW + x * p.s + dx) * p.cout + co;
+          const size_t o = (((size_t)b * OH + y * p.s + dy) * OW + x * p.s + dx) * p.ldo + co;  // ldo = channel stride
           f16x4 h;
 #pragma unroll
           for (int r = 0; r < 4; ++r) h[r] = (f16)v[r];

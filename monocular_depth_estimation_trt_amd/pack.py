@@ -49,10 +49,14 @@ def _pad2(a: np.ndarray, n_mult: int = 128, k_mult: int = 64) -> np.ndarray:
     return out
 
 
-def _conv3(w: np.ndarray) -> np.ndarray:
-    """[Cout][Cin][3][3] -> f16 [Cout_pad][9*Cin pad64] in (ky, kx, ci) order."""
+def _conv3(w: np.ndarray, cin_pad: int = 0) -> np.ndarray:
+    """[Cout][Cin][3][3] -> f16 [Cout_pad][9*Cin' pad64] in (ky, kx, ci) order,
+    Cin' = cin_pad (zero input channels appended) when given."""
     co, ci, kh, kw = w.shape
     assert kh == 3 and kw == 3, w.shape
+    if cin_pad and cin_pad > ci:
+        w = np.concatenate([w, np.zeros((co, cin_pad - ci, 3, 3), w.dtype)], axis=1)
+        ci = cin_pad
     return _pad2(np.ascontiguousarray(w.transpose(0, 2, 3, 1)).reshape(co, 9 * ci))
 
 
@@ -148,7 +152,8 @@ def packed_tensors(sd: Dict[str, np.ndarray], cfg: dict, img_h: int, img_w: int)
     o["rs3.w"] = _conv3(sd[h + "resize_layers.3.weight"])
     o["rs3.b"] = f32(sd[h + "resize_layers.3.bias"])
     for i in range(4):
-        o[f"rn{i + 1}.w"] = _conv3(sd[f"{h}scratch.layer{i + 1}_rn.weight"])
+        # DPT maps feeding the direct conv carry channels padded to x32 (48 -> 64)
+        o[f"rn{i + 1}.w"] = _conv3(sd[f"{h}scratch.layer{i + 1}_rn.weight"], -(-cfg["out_channels"][i] // 32) * 32)
     for r in range(1, 5):
         s = f"{h}scratch.refinenet{r}."
         w = sd[s + "out_conv.weight"]

@@ -56,7 +56,7 @@ def test_reference_call_sequence(gpu):
             do_inference(context, engine, bindings, inputs, outputs, stream)
             names = context.profiler.names
             context.profiler = None
-            assert "block0.attn" in names and "head.output_conv2" in names and len(names) > 100
+            assert "block0.attn" in names and "head.output_conv2" in names and len(names) > 90
             free_buffers(inputs, outputs, stream)
             b = bench.record("depth_anything_v2", samples, outputs={"depth": depth}, out_dir=os.path.join(td, "b"),
                              warmup=2, precision="fp16", input_h=98, input_w=98, engine_path=eng_path, echo=False)
