@@ -40,6 +40,12 @@
 #ifndef MDE_XCD_REMAP
 #define MDE_XCD_REMAP 1
 #endif
+#ifndef MDE_EPI_LDS
+#define MDE_EPI_LDS 1  // row-major epilogues staged through LDS (whole-line stores)
+#endif
+#ifndef MDE_GEMM_STAGES
+#define MDE_GEMM_STAGES 2  // LDS ring depth for dense A (>2: counted-vmcnt pipeline)
+#endif
 
 namespace mde {
 
@@ -52,6 +58,19 @@ MDE_DEV void glds16(const void* src, void* lds_wave_base) {
 }
 
 MDE_DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+
+template <int N>
+MDE_DEV void wait_vm_n() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Workgroup barrier that leaves LDS-DMA in flight (__syncthreads() would
+// also drain vmcnt): own LDS reads retired, raw s_barrier, compiler fences.
+MDE_DEV void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
 // LDS tile geometry for a K-step of BK halves: rows of BK*2 bytes, 16-byte
 // chunks; one glds wave-instruction (64 lanes x 16 B) fills RW rows.
@@ -184,7 +203,12 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) 
   static_assert(AINS * G::RW == BM && BINS * G::RW == BN, "tile rows vs glds rows");
   constexpr int APASS = (AINS + NW - 1) / NW, BPASS = (BINS + NW - 1) / NW;
   constexpr int STAGE = (BM + BN) * ROWB;
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  // dense A: SG-deep ring, every wave issues exactly NPER glds per stage so a
+  // counted vmcnt names "stage kt has landed"
+  constexpr int SG = (AM == A_DENSE && AINS % NW == 0 && BINS % NW == 0) ? MDE_GEMM_STAGES : 2;
+  constexpr int NPER = APASS + BPASS;
+  static_assert(SG >= 2 && SG <= 4, "stages");
+  __shared__ __attribute__((aligned(16))) char smem[SG * STAGE];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -346,13 +370,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) 
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = (p.K + BK - 1) / BK;
-  issue(0, 0);
-  commit_up(0);
-  wait_vm();
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+  auto mma_stage = [&](int cur) {
     const char* sA = smem + cur * STAGE;
     const char* sB = sA + BM * ROWB;
 #pragma unroll
@@ -377,9 +395,35 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) 
 #pragma unroll
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);
     }
-    if (kt + 1 < nk) commit_up(cur ^ 1);
+  };
+  if constexpr (SG == 2) {
+    issue(0, 0);
+    commit_up(0);
     wait_vm();
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) issue(kt + 1, cur ^ 1);
+      mma_stage(cur);
+      if (kt + 1 < nk) commit_up(cur ^ 1);
+      wait_vm();
+      __syncthreads();
+    }
+  } else {
+    // SG-1 stages in flight; one barrier per K-step.  At step kt the stages
+    // issued after kt are min(nk-1-kt, SG-2): wait until only they remain.
+#pragma unroll
+    for (int s = 0; s < SG - 1; ++s)
+      if (s < nk) issue(s, s);
+    for (int kt = 0; kt < nk; ++kt) {
+      const int after = min(nk - 1 - kt, SG - 2);
+      if (after >= 2) wait_vm_n<2 * NPER>();
+      else if (after == 1) wait_vm_n<NPER>();
+      else wait_vm_n<0>();
+      lds_barrier();  // stage kt visible to all waves; stage kt-1 fully consumed
+      if (kt + SG - 1 < nk) issue(kt + SG - 1, (kt + SG - 1) % SG);
+      mma_stage(kt % SG);
+    }
   }
 
   // ---- epilogue: lane owns (m, n..n+3) per block ----
@@ -389,7 +433,23 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) 
     const int m = m0 + wm * TM * 16 + i * 16 + (lane & 15);
     mrow[i] = m < p.M ? m : -1;
   }
-  store_tile<EM, TM, TN>(p, acc, mrow, n0 + wn * TN * 16 + (lane >> 4) * 4, lane);
+#ifdef MDE_EXP_NOEPI  // tuning experiment: main loop only (stores only if a NaN appears)
+  {
+    float z = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) z += acc[i][j][0] + acc[i][j][3];
+    if (z == z) return;
+  }
+#endif
+#if MDE_EPI_LDS
+  static_assert(BM * BN * 4 <= SG * STAGE, "LDS-staged epilogue slices");
+  if constexpr (SG > 2) lds_barrier();  // the ring's last stage may still be read by other waves
+  if (!store_tile_lds<EM, TM, TN>(p, acc, m0 + wm * TM * 16, n0 + wn * TN * 16, lane,
+                                  smem + wave * (TM * 16) * (TN * 16) * 4))
+#endif
+    store_tile<EM, TM, TN>(p, acc, mrow, n0 + wn * TN * 16 + (lane >> 4) * 4, lane);
   if constexpr (EM == E_RESID) {
     if (p.ln_counter) ln_tail<NW>(p, tm, m0, BM, ntn, smem, tid);
   }

@@ -59,7 +59,11 @@ MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&m
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
           }
+#ifdef MDE_EXP_STORE_SMALL  // tuning experiment: same stores, L2-resident target rows
+          const size_t o = (size_t)(m & 255) * p.ldo + n;
+#else
           const size_t o = (size_t)m * p.ldo + n;
+#endif
           if (p.res0) {
             const f16x4 r0 = *reinterpret_cast<const f16x4*>(reinterpret_cast<const f16*>(p.res0) + o);
 #pragma unroll
@@ -121,6 +125,115 @@ MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&m
         }
       }
     }
+  }
+}
+
+// LDS-staged epilogue for the row-major outputs (E_STORE, E_RESID and the
+// q/k thirds of E_QKV): the wave parks its (16 TM) x (16 TN) fp32 tile in its
+// own LDS slice (bias/activation applied, residuals not yet), then re-reads
+// it row-wise so that each lane owns 8 consecutive columns and every store
+// instruction writes whole 128-B lines (the direct path touches 16 partial
+// lines per instruction).  One rounding to f16, as the direct path.
+// `lds` = this wave's slice (16 TM * 16 TN * 4 bytes); m0w/n0w = the wave's
+// first output row/column; the caller has retired every LDS read of the
+// main loop (barrier) before the call.  Returns false (nothing written) for
+// modes it does not stage -- the caller then runs store_tile.
+template <int EM, int TM, int TN>
+MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], int m0w, int n0w, int lane, char* lds) {
+  constexpr int R = TM * 16, C = TN * 16;  // wave tile
+  constexpr int CHR = C / 4;               // 16-B fp32 chunks per staged row
+  constexpr int CPR = C / 8;               // lanes per row in the read-back (8 columns each)
+  constexpr int RPI = 64 / CPR;            // rows per read-back instruction
+  static_assert(TN >= 1 && C % 8 == 0, "tile");
+  if constexpr (EM != E_STORE && EM != E_RESID && EM != E_QKV) {
+    return false;
+  } else {
+    int which = 0;
+    if constexpr (EM == E_QKV) {
+      which = n0w / (p.heads * 64);
+      if (which == 2 || (n0w & 63) + C > 64) return false;  // V^T keeps the transposing direct path
+    }
+    auto phys = [&](int row, int ch) { return row * (C * 4) + ((ch ^ (row & (CHR >= 8 ? 7 : CHR - 1))) << 4); };
+    // ---- phase 1: accumulators (+bias, activation) -> LDS ----
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = n0w + j * 16 + (lane >> 4) * 4;
+      float4 bn = {0.f, 0.f, 0.f, 0.f};
+      if (p.bias && n < p.N) bn = *reinterpret_cast<const float4*>(p.bias + n);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        f32x4 v = acc[i][j];
+        v[0] += bn.x; v[1] += bn.y; v[2] += bn.z; v[3] += bn.w;
+        if constexpr (EM == E_STORE) {
+          if (p.act == ACT_RELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+          } else if (p.act == ACT_GELU) {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
+          }
+        }
+        const int row = i * 16 + (lane & 15);
+        *reinterpret_cast<f32x4*>(lds + phys(row, j * 4 + (lane >> 4))) = v;
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // ---- phase 2: whole rows out ----
+    const int rr = lane / CPR, cc = lane - (lane / CPR) * CPR;
+    const int n = n0w + cc * 8;
+    if (n >= p.N) return true;
+    float4 ls0 = {0.f, 0.f, 0.f, 0.f}, ls1 = ls0;
+    if constexpr (EM == E_RESID) {
+      ls0 = *reinterpret_cast<const float4*>(p.ls + n);
+      ls1 = *reinterpret_cast<const float4*>(p.ls + n + 4);
+    }
+#pragma unroll
+    for (int it = 0; it < (R + RPI - 1) / RPI; ++it) {
+      const int row = it * RPI + rr;
+      if (R % RPI != 0 && row >= R) break;
+      const int m = m0w + row;
+      if (m >= p.M) break;
+      const f32x4 a = *reinterpret_cast<const f32x4*>(lds + phys(row, 2 * cc));
+      const f32x4 b = *reinterpret_cast<const f32x4*>(lds + phys(row, 2 * cc + 1));
+      float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+      if constexpr (EM == E_STORE) {
+        const size_t o = (size_t)m * p.ldo + n;
+        if (p.res0) {
+          const f16x8 r0 = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res0) + o);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) v[r] += (float)r0[r];
+        }
+        if (p.res1) {
+          const f16x8 r1 = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res1) + o);
+#pragma unroll
+          for (int r = 0; r < 8; ++r) v[r] += (float)r1[r];
+        }
+        f16x8 h;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) h[r] = (f16)v[r];
+        *reinterpret_cast<f16x8*>(reinterpret_cast<f16*>(p.out16) + o) = h;
+      } else if constexpr (EM == E_RESID) {
+        float4* x = reinterpret_cast<float4*>(p.x32 + (size_t)m * p.ldo + n);
+        float4 x0 = x[0], x1 = x[1];
+        x0.x += ls0.x * v[0]; x0.y += ls0.y * v[1]; x0.z += ls0.z * v[2]; x0.w += ls0.w * v[3];
+        x1.x += ls1.x * v[4]; x1.y += ls1.y * v[5]; x1.z += ls1.z * v[6]; x1.w += ls1.w * v[7];
+        x[0] = x0;
+        x[1] = x1;
+      } else {  // E_QKV, q or k third
+        const int D = p.heads * 64, w = n - which * D;
+        const int b = m / p.T, t = m - (m / p.T) * p.T;
+        const size_t bh = (size_t)b * p.heads + (w >> 6);
+        const float sc = which == 0 ? p.qscale : 1.f;
+        f16x8 h;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) h[r] = (f16)(v[r] * sc);
+        f16* dst = (which == 0 ? reinterpret_cast<f16*>(p.q) : reinterpret_cast<f16*>(p.k)) +
+                   (bh * p.Tpad + t) * 64 + (w & 63);
+        *reinterpret_cast<f16x8*>(dst) = h;
+      }
+    }
+    return true;
   }
 }
 
