@@ -18,6 +18,10 @@
 #include "mde_ops.h"
 #include "tile_epilogue.h"
 
+#ifndef MDE_EPI_LDS
+#define MDE_EPI_LDS 1  // row-major epilogue staged through LDS (whole-line stores)
+#endif
+
 namespace mde {
 
 namespace {
@@ -52,7 +56,9 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3_kernel(const GemmParams p)
   constexpr int BSTAGE = BN * ROWB;
   constexpr int BINS = BN / RWP;                              // B rows per wave-instruction = RWP
   static_assert(BINS * RWP == BN, "B tile rows");
-  __shared__ __attribute__((aligned(16))) char smem[PATCH + 2 * BSTAGE];
+  // the LDS-staged epilogue reuses the patch/B space for the fp32 tile
+  constexpr int MAIN = PATCH + 2 * BSTAGE, EPI = MDE_EPI_LDS ? BM * BN * 4 : 0;
+  __shared__ __attribute__((aligned(16))) char smem[MAIN > EPI ? MAIN : EPI];
   char* sP = smem;
   char* sB0 = smem + PATCH;
 
@@ -185,7 +191,17 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3_kernel(const GemmParams p)
     const int oy = ty * TH + wm * TM + i, ox = tx * TW + (lane & 15);
     mrow[i] = (oy < Ho && ox < Wo) ? ((b * Ho + oy) * Wo + ox) : -1;
   }
-  store_tile<EM, TM, TN>(p, acc, mrow, n0 + wn * TN * 16 + (lane >> 4) * 4, lane);
+#if MDE_EPI_LDS
+  // the main loop ended on a barrier: the LDS is free
+  if (!store_tile_lds<EM, TM, TN>(
+          p, acc,
+          [&](int row) {
+            const int oy = ty * TH + wm * TM + (row >> 4), ox = tx * TW + (row & 15);
+            return (oy < Ho && ox < Wo) ? ((b * Ho + oy) * Wo + ox) : -1;
+          },
+          n0 + wn * TN * 16, lane, smem + wave * (TM * 16) * (TN * 16) * 4))
+#endif
+    store_tile<EM, TM, TN>(p, acc, mrow, n0 + wn * TN * 16 + (lane >> 4) * 4, lane);
 }
 
 template <int BN, int WM, int WN, int CK, int S, bool UP, int EM>

@@ -446,8 +446,10 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) 
 #if MDE_EPI_LDS
   static_assert(BM * BN * 4 <= SG * STAGE, "LDS-staged epilogue slices");
   if constexpr (SG > 2) lds_barrier();  // the ring's last stage may still be read by other waves
-  if (!store_tile_lds<EM, TM, TN>(p, acc, m0 + wm * TM * 16, n0 + wn * TN * 16, lane,
-                                  smem + wave * (TM * 16) * (TN * 16) * 4))
+  const int m0w = m0 + wm * TM * 16;
+  if (!store_tile_lds<EM, TM, TN>(
+          p, acc, [&](int row) { return m0w + row < p.M ? m0w + row : -1; }, n0 + wn * TN * 16, lane,
+          smem + wave * (TM * 16) * (TN * 16) * 4))
 #endif
     store_tile<EM, TM, TN>(p, acc, mrow, n0 + wn * TN * 16 + (lane >> 4) * 4, lane);
   if constexpr (EM == E_RESID) {

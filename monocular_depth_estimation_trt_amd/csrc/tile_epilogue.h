@@ -134,12 +134,13 @@ MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&m
 // it row-wise so that each lane owns 8 consecutive columns and every store
 // instruction writes whole 128-B lines (the direct path touches 16 partial
 // lines per instruction).  One rounding to f16, as the direct path.
-// `lds` = this wave's slice (16 TM * 16 TN * 4 bytes); m0w/n0w = the wave's
-// first output row/column; the caller has retired every LDS read of the
-// main loop (barrier) before the call.  Returns false (nothing written) for
-// modes it does not stage -- the caller then runs store_tile.
-template <int EM, int TM, int TN>
-MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], int m0w, int n0w, int lane, char* lds) {
+// `lds` = this wave's slice (16 TM * 16 TN * 4 bytes); mof(row) = output row
+// of wave-tile row `row` (or -1), n0w = the wave's first output column; the
+// caller has retired every LDS read of the main loop (barrier) before the
+// call.  Returns false (nothing written) for modes it does not stage -- the
+// caller then runs store_tile.
+template <int EM, int TM, int TN, class RowMap>
+MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mof, int n0w, int lane, char* lds) {
   constexpr int R = TM * 16, C = TN * 16;  // wave tile
   constexpr int CHR = C / 4;               // 16-B fp32 chunks per staged row
   constexpr int CPR = C / 8;               // lanes per row in the read-back (8 columns each)
@@ -192,8 +193,8 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], int m0w, 
     for (int it = 0; it < (R + RPI - 1) / RPI; ++it) {
       const int row = it * RPI + rr;
       if (R % RPI != 0 && row >= R) break;
-      const int m = m0w + row;
-      if (m >= p.M) break;
+      const int m = mof(row);
+      if (m < 0) continue;
       const f32x4 a = *reinterpret_cast<const f32x4*>(lds + phys(row, 2 * cc));
       const f32x4 b = *reinterpret_cast<const f32x4*>(lds + phys(row, 2 * cc + 1));
       float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};

@@ -9,4 +9,4 @@ for v in base noldsepi; do
   timeout -k 10 120 python tools/bench_kernels.py --lib $lib --iters 30 >> gpurun_out/kv.log 2>&1
 done
 timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/kv_tests.log 2>&1
-timeout -k 10 300 python bench.py > gpurun_out/bench7.json 2> gpurun_out/bench7.err
+timeout -k 10 300 python bench.py > gpurun_out/bench8.json 2> gpurun_out/bench8.err
