@@ -16,7 +16,9 @@ Also measured (rank 0):
   * b1_*: the reference's own methodology (core/bench.py:182-210): batch 1,
     wall clock of one do_inference() = pinned H2D + forward + D2H + sync,
     20 warmup / 100 iterations, with the StageTimer split -- the number to
-    hold against the RTX-3080 TensorRT 4.31 ms / 232.11 FPS.
+    hold against the RTX-3080 TensorRT 4.31 ms / 232.11 FPS (BASELINE.md);
+    b1_u8_*: the same with the uint8-NHWC engine (on-device normalisation),
+    against the reference's uint8 A/B 294.07 FPS.
   * roofline: the dominant layer class (largest share of forward time), its
     algorithmic FLOP per launch / its average launch time, timed live with
     hipEvents on the engine's stream (the engine profiler), vs the dense
@@ -41,6 +43,7 @@ sys.path.insert(0, ROOT)
 
 MFMA_PEAK_TFLOPS = 2500.0   # dense fp16/bf16 MFMA, MI355X (MI355X_MICROARCH.md chip table)
 REF_B1_FPS = 232.11         # RTX 3080 TRT fp16, BASELINE.md
+REF_B1_U8_FPS = 294.07      # same, uint8-NHWC input engine (reports/uint8_ab/depth_anything_v2.json)
 
 
 def log(*a):
@@ -107,15 +110,17 @@ def roofline(cfg, B, size, layer_ms):
             "launches_per_step": cls_n[dom]}, breakdown
 
 
-def b1_reference_method(blob, dev, size, warmup, iters):
-    """Batch-1 wall clock exactly as core/bench.py measures the TRT engine."""
+def b1_reference_method(blob, dev, size, warmup, iters, u8=False, prefix="b1_"):
+    """Batch-1 wall clock exactly as core/bench.py measures the TRT engine.
+    u8: the uint8-NHWC engine (the reference's A/B, reports/uint8_ab/
+    depth_anything_v2.json: 294.07 FPS on the 3080), 0.8 MB H2D."""
     from monocular_depth_estimation_trt_amd import common_runtime as cr
     from monocular_depth_estimation_trt_amd import weights
     from monocular_depth_estimation_trt_amd.engine import Engine
     eng = Engine.from_bytes(blob, dev)
     ctx = eng.create_execution_context()
     inputs, outputs, bindings, stream = cr.allocate_buffers(eng, None, profile_idx=0)
-    inputs[0].host = weights.synthetic_images(1, size, size, first_seed=0)
+    inputs[0].host = (weights.synthetic_images_u8 if u8 else weights.synthetic_images)(1, size, size, first_seed=0)
     timer = cr.StageTimer()
     fn = lambda: cr.do_inference(ctx, eng, bindings, inputs, outputs, stream, timer=timer)  # noqa: E731
     for _ in range(warmup):
@@ -135,12 +140,13 @@ def b1_reference_method(blob, dev, size, warmup, iters):
     mean = statistics.fmean(samples)
     s = sorted(samples)
     pct = lambda q: s[min(len(s) - 1, max(0, int(np.ceil(q / 100 * len(s))) - 1))]  # noqa: E731
-    res = {"b1_mean_ms": round(mean, 4), "b1_p50_ms": round(pct(50), 4), "b1_p99_ms": round(pct(99), 4),
-           "b1_fps": round(1000.0 / mean, 2), "b1_vs_ref_fps": round(1000.0 / mean / REF_B1_FPS, 3)}
+    ref = REF_B1_U8_FPS if u8 else REF_B1_FPS
+    res = {"mean_ms": round(mean, 4), "p50_ms": round(pct(50), 4), "p99_ms": round(pct(99), 4),
+           "fps": round(1000.0 / mean, 2), "vs_ref_fps": round(1000.0 / mean / ref, 3)}
     for k, v in stages.items():
-        res["b1_" + k] = round(statistics.fmean(v), 4)
-    res["b1_out_mean"] = float(out.mean())
-    return res
+        res[k] = round(statistics.fmean(v), 4)
+    res["out_mean"] = float(out.mean())
+    return {prefix + k: v for k, v in res.items()}
 
 
 def cpu_baseline(cfg, size, seconds):
@@ -222,6 +228,9 @@ def main():
     gflop = total_flops(cfg, S, S) / 1e9
     model_frac = value / world * gflop * 1e9 / (MFMA_PEAK_TFLOPS * 1e12)
     res_b1 = {} if a.no_b1 else b1_reference_method(blob, local, S, a.b1_warmup, a.b1_iters)
+    if not a.no_b1:
+        blob_u8 = pack.pack_bytes(sd, cfg, S, S, input_format="uint8_nhwc")
+        res_b1.update(b1_reference_method(blob_u8, local, S, a.b1_warmup, a.b1_iters, u8=True, prefix="b1_u8_"))
     ctx.destroy()
     eng.destroy()
     cpu = None

@@ -38,7 +38,7 @@
 extern "C" {
 #endif
 
-#define MDE_ABI_VERSION 1
+#define MDE_ABI_VERSION 2
 
 typedef enum {
   MDE_OK = 0,
@@ -52,7 +52,7 @@ typedef enum {
 } mde_status;
 
 /* Same numbering as tensorrt.DataType for the types used here. */
-typedef enum { MDE_FLOAT32 = 0, MDE_FLOAT16 = 1 } mde_dtype;
+typedef enum { MDE_FLOAT32 = 0, MDE_FLOAT16 = 1, MDE_UINT8 = 5 } mde_dtype; /* tensorrt.DataType values */
 
 typedef struct mde_engine mde_engine;
 typedef struct mde_context mde_context;
@@ -73,6 +73,7 @@ typedef struct {
   float max_depth, ln_eps;
   int32_t max_batch_hint;
   int64_t weight_bytes;
+  int32_t input_format; /* 0: "input" float32 NCHW [B,3,H,W]; 1: "image_u8" uint8 NHWC [B,H,W,3] */
 } mde_engine_info;
 
 /* IProfiler.report_layer_time analogue: one call per launched layer. */
@@ -163,6 +164,15 @@ int mde_op_resize_bilinear(const void* in_f16, int batch, int ih, int iw, int c,
 int mde_op_depth_head(const void* in_f16, int batch, int sh, int sw, int cin, int uh, int uw, const void* w_f16,
                       int ldw, const float* bias, const float* w2, float b2, int metric, float max_depth,
                       float* out_f32, void* stream);
+/* uint8 NHWC image [batch][h][w][3] -> the patch-embed operand [batch*(h/14)*(w/14)][672] f16
+ * (patch-major, channel, row, 16-wide padded column), computing ((float)u / scale - mean[c]) / std[c]
+ * in fp32 (the ONNX preamble of reference core/onnx_tools.py:175-199: Cast, Div, Sub, Div). */
+int mde_op_patch_prep_u8(const unsigned char* img_u8, int batch, int h, int w, float scale, const float* mean3,
+                         const float* std3, void* patches_f16, void* stream);
+/* Post-process (reference models/depth_anything_v2/onnx2trt.py:111-117): bilinear
+ * align_corners=True resize of fp32 depth [batch][ih][iw] to [batch][oh][ow], then clamp to [lo, hi]. */
+int mde_op_depth_postprocess(const float* depth, int batch, int ih, int iw, float* out, int oh, int ow, float lo,
+                             float hi, void* stream);
 
 #ifdef __cplusplus
 }

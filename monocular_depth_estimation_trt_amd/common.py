@@ -81,12 +81,13 @@ def _infer_encoder(sd: dict) -> str:
 
 
 def _engine_fingerprint(src, precision, workspace_gib, opt_level, obey_precision_constraints,
-                        dynamic_input_shapes, encoder, depth_type, max_depth, input_hw) -> str:
+                        dynamic_input_shapes, encoder, depth_type, max_depth, input_hw,
+                        input_format="float32_nchw") -> str:
     parts = [_source_digest(src), f"packer={pack.PACKER_VERSION}", f"precision={precision}",
              f"workspace={workspace_gib}", f"opt_level={opt_level}",
              f"obey_precision={obey_precision_constraints}", f"dynamic={dynamic_input_shapes}",
              f"encoder={encoder}", f"depth_type={depth_type}", f"max_depth={max_depth}",
-             f"input_hw={tuple(input_hw)}", "arch=gfx950"]
+             f"input_hw={tuple(input_hw)}", f"input_format={input_format}", "arch=gfx950"]
     return "\n".join(parts)
 
 
@@ -111,7 +112,7 @@ def get_engine(onnx_file_path, engine_file_path="", precision="fp32", dynamic_in
                workspace_gib=2, opt_level=None, obey_precision_constraints=False, check_fingerprint=True,
                *, encoder: Optional[str] = None, depth_type: Optional[str] = None,
                max_depth: Optional[float] = None, input_hw: Optional[Sequence[int]] = None,
-               device: int = 0) -> Engine:
+               input_format: str = "float32_nchw", device: int = 0) -> Engine:
     """Load `engine_file_path` if it matches its source, otherwise pack it.
 
     `onnx_file_path` keeps the reference's parameter name; it names the
@@ -120,7 +121,13 @@ def get_engine(onnx_file_path, engine_file_path="", precision="fp32", dynamic_in
     dynamic-batch engine whose contexts are sized for max[0].
     `precision`: "fp16" (the engine's arithmetic: f16 operands, fp32
     accumulation/statistics).  "fp32" raises -- there is no fp32 engine.
+    `input_format` "uint8_nhwc" packs the reference's uint8 preamble
+    (core/onnx_tools.py:87-219): the input binding becomes "image_u8",
+    uint8 [B,H,W,3], normalised on the device.
     """
+    if input_format not in pack.INPUT_FORMATS:
+        raise ValueError(f"[MDET] input_format must be one of {pack.INPUT_FORMATS}")
+    u8 = input_format == "uint8_nhwc"
     src = str(onnx_file_path)
     if precision not in ("fp16", "fp32"):
         raise ValueError(f"[MDET] unknown precision {precision!r}")
@@ -133,7 +140,7 @@ def get_engine(onnx_file_path, engine_file_path="", precision="fp32", dynamic_in
             raise ValueError("[MDET] only the batch dimension may be dynamic")
         if not (1 <= mn[0] <= opt[0] <= mx[0]):
             raise ValueError(f"[MDET] bad batch profile {mn[0]}/{opt[0]}/{mx[0]}")
-        input_hw = input_hw or (mn[2], mn[3])
+        input_hw = input_hw or ((mn[1], mn[2]) if u8 else (mn[2], mn[3]))
         profile = (mn, opt, mx)
     else:
         profile = None
@@ -154,7 +161,8 @@ def get_engine(onnx_file_path, engine_file_path="", precision="fp32", dynamic_in
     present = source_exists(src)
     if check_fingerprint and present and engine_file_path:
         fingerprint = _engine_fingerprint(src, precision, workspace_gib, opt_level, obey_precision_constraints,
-                                          dynamic_input_shapes, encoder, depth_type, max_depth, input_hw)
+                                          dynamic_input_shapes, encoder, depth_type, max_depth, input_hw,
+                                          input_format)
 
     def build_engine() -> bytes:
         nonlocal sd, encoder
@@ -167,7 +175,7 @@ def get_engine(onnx_file_path, engine_file_path="", precision="fp32", dynamic_in
             sd = load_checkpoint(src)
             encoder = encoder or _infer_encoder(sd)
             cfg = weights.model_config(encoder, depth_type, max_depth)
-        return pack.pack_bytes(sd, cfg, *input_hw)
+        return pack.pack_bytes(sd, cfg, *input_hw, input_format=input_format)
 
     kw = dict(profile=profile, static_batch=1)
     if engine_file_path:

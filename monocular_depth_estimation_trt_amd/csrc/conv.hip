@@ -88,8 +88,8 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3_kernel(const GemmParams p)
 
   float usy = 0.f, usx = 0.f;
   if constexpr (UP) {
-    usy = p.uh > 1 ? (float)(p.ch - 1) / (float)(p.uh - 1) : 0.f;
-    usx = p.uw > 1 ? (float)(p.cw - 1) / (float)(p.uw - 1) : 0.f;
+    usy = ac_scale(p.ch, p.uh);
+    usx = ac_scale(p.cw, p.uw);
   }
 
   auto load_patch = [&](int chunk) {
@@ -110,11 +110,10 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3_kernel(const GemmParams p)
         const int iy = iy0 + py, ix = ix0 + px;
         f16x8 v = zero8();
         if (iy >= 0 && iy < IH && ix >= 0 && ix < IW) {
-          const float fy = usy * (float)iy, fx = usx * (float)ix;
-          const int y0 = (int)fy, x0 = (int)fx;
-          const int y1 = y0 + (y0 < p.ch - 1 ? 1 : 0), x1 = x0 + (x0 < p.cw - 1 ? 1 : 0);
-          const float ly1 = fy - (float)y0, ly0 = 1.f - ly1;
-          const float lx1 = fx - (float)x0, lx0 = 1.f - lx1;
+          int y0, y1, x0, x1;
+          float ly0, ly1, lx0, lx1;
+          ac_index(usy, iy, p.ch, y0, y1, ly0, ly1);
+          ac_index(usx, ix, p.cw, x0, x1, lx0, lx1);
           const f16* base = img + cbase + lc * 8;
           const f16x8 a = *reinterpret_cast<const f16x8*>(base + ((size_t)y0 * p.cw + x0) * p.cc);
           const f16x8 bq = *reinterpret_cast<const f16x8*>(base + ((size_t)y0 * p.cw + x1) * p.cc);

@@ -82,6 +82,77 @@ __global__ void __launch_bounds__(256) patch_prep_kernel(const float* __restrict
   }
 }
 
+// uint8 NHWC variant of patch_prep_kernel: the reference's uint8 preamble
+// (core/onnx_tools.py:175-199: Cast -> Div(scale) -> Sub(mean) -> Div(std),
+// all fp32) fused into the patch gather.  One thread per (patch, kernel row,
+// 8-column half): 8 pixels x 3 channels, three 16-byte chunk stores.  The
+// IEEE ops are spelled out (__fdiv_rn / __fsub_rn) so no FMA contraction
+// changes the bits against the host preprocessing.
+struct InNorm {
+  float scale, mean[3], stdv[3];
+};
+
+__global__ void __launch_bounds__(256) patch_prep_u8_kernel(const unsigned char* __restrict__ img, f16* __restrict__ P,
+                                                            float* __restrict__ X, const float* __restrict__ cls_pos,
+                                                            int B, int H, int W, int ph, int pw, int T, int D,
+                                                            InNorm nrm) {
+  const long long np = (long long)ph * pw;
+  const long long nchunk = (long long)B * np * 28;  // 14 rows x 2 halves
+  long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id < nchunk) {
+    const long long patch = id / 28;
+    const int r = (int)(id - patch * 28);
+    const int ky = r >> 1, half = r & 1;
+    const int b = (int)(patch / np);
+    const int pi = (int)(patch - (long long)b * np);
+    const int py = pi / pw, px = pi - (pi / pw) * pw;
+    const unsigned char* src = img + (((size_t)b * H + py * 14 + ky) * W + px * 14 + half * 8) * 3;
+    const int nvalid = half ? 6 : 8;
+    f16x8 v[3];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+#pragma unroll
+      for (int c = 0; c < 3; ++c) {
+        float f = 0.f;
+        if (j < nvalid) {
+          f = __fdiv_rn((float)src[j * 3 + c], nrm.scale);
+          f = __fdiv_rn(__fsub_rn(f, nrm.mean[c]), nrm.stdv[c]);
+        }
+        v[c][j] = (f16)f;
+      }
+#pragma unroll
+    for (int c = 0; c < 3; ++c) *reinterpret_cast<f16x8*>(P + patch * PK + c * 224 + ky * 16 + half * 8) = v[c];
+    return;
+  }
+  id -= nchunk;
+  if (X && id < (long long)B * D) {
+    const int b = (int)(id / D), d = (int)(id - (long long)(id / D) * D);
+    X[(size_t)b * T * D + d] = cls_pos[d];
+  }
+}
+
+// Depth post-process: PyTorch upsample_bilinear2d(align_corners=True) of one
+// fp32 channel, then clamp (reference onnx2trt.py:111-117).  One thread per
+// output pixel, fp32 index math exactly as resize_kernel below.
+__global__ void __launch_bounds__(256) depth_post_kernel(const float* __restrict__ in, float* __restrict__ out, int B,
+                                                         int ih, int iw, int oh, int ow, float lo, float hi) {
+  const long long n = (long long)B * oh * ow;
+  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (id >= n) return;
+  const int ox = (int)(id % ow);
+  const long long q = id / ow;
+  const int oy = (int)(q % oh);
+  const int b = (int)(q / oh);
+  int y0, y1, x0, x1;
+  float ly0, ly1, lx0, lx1;
+  ac_index(ac_scale(ih, oh), oy, ih, y0, y1, ly0, ly1);
+  ac_index(ac_scale(iw, ow), ox, iw, x0, x1, lx0, lx1);
+  const float* s = in + (size_t)b * ih * iw;
+  const float v = ly0 * (lx0 * s[(size_t)y0 * iw + x0] + lx1 * s[(size_t)y0 * iw + x1]) +
+                  ly1 * (lx0 * s[(size_t)y1 * iw + x0] + lx1 * s[(size_t)y1 * iw + x1]);
+  out[id] = fminf(fmaxf(v, lo), hi);
+}
+
 // PyTorch upsample_bilinear2d(align_corners=True): src = dst*(in-1)/(out-1),
 // h1 = floor(src), h1p = (h1 < in-1), lambda = src - h1; fp32 arithmetic.
 __global__ void __launch_bounds__(256) resize_kernel(const f16* __restrict__ in, f16* __restrict__ out, int B,
@@ -96,13 +167,10 @@ __global__ void __launch_bounds__(256) resize_kernel(const f16* __restrict__ in,
   pix /= ow;
   const int oy = (int)(pix % oh);
   const int b = (int)(pix / oh);
-  const float sy = oh > 1 ? (float)(ih - 1) / (float)(oh - 1) : 0.f;
-  const float sx = ow > 1 ? (float)(iw - 1) / (float)(ow - 1) : 0.f;
-  const float fy = sy * (float)oy, fx = sx * (float)ox;
-  const int y0 = (int)fy, x0 = (int)fx;
-  const int y1 = y0 + (y0 < ih - 1 ? 1 : 0), x1 = x0 + (x0 < iw - 1 ? 1 : 0);
-  const float ly1 = fy - (float)y0, ly0 = 1.f - ly1;
-  const float lx1 = fx - (float)x0, lx0 = 1.f - lx1;
+  int y0, y1, x0, x1;
+  float ly0, ly1, lx0, lx1;
+  ac_index(ac_scale(ih, oh), oy, ih, y0, y1, ly0, ly1);
+  ac_index(ac_scale(iw, ow), ox, iw, x0, x1, lx0, lx1);
   const f16* base = in + (size_t)b * ih * iw * C + c8 * 8;
   const f16x8 a = *reinterpret_cast<const f16x8*>(base + ((size_t)y0 * iw + x0) * C);
   const f16x8 bb = *reinterpret_cast<const f16x8*>(base + ((size_t)y0 * iw + x1) * C);
@@ -137,6 +205,32 @@ hipError_t launch_patch_prep(const float* img, h16* P, float* X, const float* cl
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(patch_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, img,
                      reinterpret_cast<f16*>(P), X, cls_pos, B, H, W, ph, pw, T, D);
+  return hipGetLastError();
+}
+
+hipError_t launch_patch_prep_u8(const unsigned char* img, h16* P, float* X, const float* cls_pos, int B, int H, int W,
+                                int ph, int pw, int T, int D, float scale, const float* mean3, const float* std3,
+                                hipStream_t st) {
+  if (ph < 1 || pw < 1 || H < ph * 14 || W < pw * 14 || scale == 0.f) return hipErrorInvalidValue;
+  const long long n = (long long)B * ph * pw * 28 + (X ? (long long)B * D : 0);
+  if (n <= 0) return hipSuccess;
+  InNorm nrm;
+  nrm.scale = scale;
+  for (int c = 0; c < 3; ++c) {
+    nrm.mean[c] = mean3[c];
+    nrm.stdv[c] = std3[c];
+  }
+  hipLaunchKernelGGL(patch_prep_u8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, img,
+                     reinterpret_cast<f16*>(P), X, cls_pos, B, H, W, ph, pw, T, D, nrm);
+  return hipGetLastError();
+}
+
+hipError_t launch_depth_postprocess(const float* in, int B, int ih, int iw, float* out, int oh, int ow, float lo,
+                                    float hi, hipStream_t st) {
+  if (ih < 1 || iw < 1 || oh < 1 || ow < 1 || B < 1) return hipErrorInvalidValue;
+  const long long n = (long long)B * oh * ow;
+  hipLaunchKernelGGL(depth_post_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, out, B, ih, iw, oh,
+                     ow, lo, hi);
   return hipGetLastError();
 }
 

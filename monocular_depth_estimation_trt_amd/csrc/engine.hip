@@ -132,6 +132,9 @@ int load_pack(const uint8_t* data, size_t n, int device, mde_engine** out) {
       c.img_h <= 0 || c.img_w <= 0 || c.features % 16 || c.head_hidden != 32) {
     delete e;
     return fail(MDE_ERR_FORMAT, "unsupported model geometry in packed config");
+  if (c.input_u8 != 0 && c.input_u8 != 1) return fail(MDE_ERR_FORMAT, "bad input format in packed config");
+  if (c.input_u8 && (c.in_scale == 0.f || c.in_std[0] == 0.f || c.in_std[1] == 0.f || c.in_std[2] == 0.f))
+    return fail(MDE_ERR_FORMAT, "uint8 input preamble with a zero scale/std");
   }
   hipError_t he = hipSetDevice(device);
   if (he != hipSuccess) {
@@ -379,7 +382,7 @@ struct Runner {
     if (dst) step((p + ".resize").c_str(), [&] { return launch_resize(c.b.vb, dst, B, h, w, F, oh, ow, st); });
   }
 
-  hipError_t forward(int B, const float* img, float* out) {
+  hipError_t forward(int B, const void* img, float* out) {
     mde_engine& e = *c.e;
     const PackConfig& cf = e.cfg;
     const int D = e.D, T = e.T, np = e.np, F = e.F;
@@ -387,7 +390,11 @@ struct Runner {
     Buf& b = c.b;
 
     step("patch_prep", [&] {
-      return launch_patch_prep(img, b.P, b.X, w32("pos.cls"), B, cf.img_h, cf.img_w, e.ph, e.pw, T, D, st);
+      if (cf.input_u8)
+        return launch_patch_prep_u8((const unsigned char*)img, b.P, b.X, w32("pos.cls"), B, cf.img_h, cf.img_w, e.ph,
+                                    e.pw, T, D, cf.in_scale, cf.in_mean, cf.in_std, st);
+      return launch_patch_prep((const float*)img, b.P, b.X, w32("pos.cls"), B, cf.img_h, cf.img_w, e.ph, e.pw, T, D,
+                               st);
     });
     {
       GemmParams g = dense(b.P, 672, "patch.w", B * np, D, 672);
@@ -619,7 +626,8 @@ int check_ctx(const mde_context* c) {
   return MDE_OK;
 }
 
-bool is_input(const char* n) { return n && strcmp(n, "input") == 0; }
+const char* input_name(const mde_engine* e) { return e->cfg.input_u8 ? "image_u8" : "input"; }
+bool is_input(const mde_engine* e, const char* n) { return n && strcmp(n, input_name(e)) == 0; }
 bool is_output(const char* n) { return n && strcmp(n, "output") == 0; }
 
 }  // namespace
@@ -697,6 +705,7 @@ int mde_engine_get_info(const mde_engine* e, mde_engine_info* o) {
   o->ln_eps = c.ln_eps;
   o->max_batch_hint = 64;
   o->weight_bytes = (int64_t)e->wbytes;
+  o->input_format = c.input_u8 ? 1 : 0;
   return MDE_OK;
 }
 
@@ -709,7 +718,16 @@ int mde_engine_num_io(const mde_engine* e, int* n) {
 int mde_engine_io_desc(const mde_engine* e, int index, mde_io_desc* o) {
   if (!e || !o) return fail(MDE_ERR_ARG, "null argument");
   memset(o, 0, sizeof *o);
-  if (index == 0) {
+  if (index == 0 && e->cfg.input_u8) {
+    strcpy(o->name, "image_u8");
+    o->dtype = MDE_UINT8;
+    o->is_input = 1;
+    o->rank = 4;
+    o->dims[0] = -1;
+    o->dims[1] = e->cfg.img_h;
+    o->dims[2] = e->cfg.img_w;
+    o->dims[3] = 3;
+  } else if (index == 0) {
     strcpy(o->name, "input");
     o->dtype = MDE_FLOAT32;
     o->is_input = 1;
@@ -737,7 +755,7 @@ int mde_engine_profile_shape(const mde_engine* e, const char* name, int which, i
   if (which < 0 || which > 2) return fail(MDE_ERR_ARG, "which must be 0 (min), 1 (opt) or 2 (max)");
   const int64_t bsel[3] = {1, 1, 64};
   mde_io_desc d;
-  int idx = is_input(name) ? 0 : is_output(name) ? 1 : -1;
+  int idx = is_input(e, name) ? 0 : is_output(name) ? 1 : -1;
   if (idx < 0) return fail(MDE_ERR_NAME, std::string("unknown tensor ") + name);
   mde_engine_io_desc(e, idx, &d);
   *rank = d.rank;
@@ -794,7 +812,7 @@ int mde_context_destroy(mde_context* c) {
 
 int mde_context_set_tensor_address(mde_context* c, const char* name, void* ptr) {
   if (int rc = check_ctx(c)) return rc;
-  if (is_input(name)) c->in = ptr;
+  if (is_input(c->e, name)) c->in = ptr;
   else if (is_output(name)) c->out = ptr;
   else return fail(MDE_ERR_NAME, std::string("unknown tensor ") + (name ? name : "(null)"));
   return MDE_OK;
@@ -802,12 +820,19 @@ int mde_context_set_tensor_address(mde_context* c, const char* name, void* ptr) 
 
 int mde_context_set_input_shape(mde_context* c, const char* name, const int64_t* dims, int rank) {
   if (int rc = check_ctx(c)) return rc;
-  if (!is_input(name)) return fail(MDE_ERR_NAME, std::string("not an input: ") + (name ? name : "(null)"));
-  if (!dims || rank != 4) return fail(MDE_ERR_SHAPE, "input shape must be rank 4 [B,3,H,W]");
+  if (!is_input(c->e, name)) return fail(MDE_ERR_NAME, std::string("not an input: ") + (name ? name : "(null)"));
   const PackConfig& cf = c->e->cfg;
-  if (dims[1] != 3 || dims[2] != cf.img_h || dims[3] != cf.img_w)
-    return fail(MDE_ERR_SHAPE, "input shape must be [B,3," + std::to_string(cf.img_h) + "," +
-                                   std::to_string(cf.img_w) + "] for this engine");
+  if (cf.input_u8) {
+    if (!dims || rank != 4) return fail(MDE_ERR_SHAPE, "input shape must be rank 4 [B,H,W,3]");
+    if (dims[3] != 3 || dims[1] != cf.img_h || dims[2] != cf.img_w)
+      return fail(MDE_ERR_SHAPE, "input shape must be [B," + std::to_string(cf.img_h) + "," +
+                                     std::to_string(cf.img_w) + ",3] for this engine");
+  } else {
+    if (!dims || rank != 4) return fail(MDE_ERR_SHAPE, "input shape must be rank 4 [B,3,H,W]");
+    if (dims[1] != 3 || dims[2] != cf.img_h || dims[3] != cf.img_w)
+      return fail(MDE_ERR_SHAPE, "input shape must be [B,3," + std::to_string(cf.img_h) + "," +
+                                     std::to_string(cf.img_w) + "] for this engine");
+  }
   if (dims[0] < 1 || dims[0] > c->max_batch)
     return fail(MDE_ERR_SHAPE, "batch " + std::to_string(dims[0]) + " outside [1, " +
                                    std::to_string(c->max_batch) + "]");
@@ -819,7 +844,7 @@ int mde_context_get_tensor_shape(const mde_context* c, const char* name, int64_t
   if (int rc = check_ctx(c)) return rc;
   if (!dims || !rank) return fail(MDE_ERR_ARG, "null argument");
   mde_io_desc d;
-  int idx = is_input(name) ? 0 : is_output(name) ? 1 : -1;
+  int idx = is_input(c->e, name) ? 0 : is_output(name) ? 1 : -1;
   if (idx < 0) return fail(MDE_ERR_NAME, std::string("unknown tensor ") + (name ? name : "(null)"));
   mde_engine_io_desc(c->e, idx, &d);
   *rank = d.rank;
@@ -853,7 +878,7 @@ int mde_context_enqueue(mde_context* c, void* stream) {
   if (!c->in || !c->out) return fail(MDE_ERR_STATE, "set_tensor_address('input'/'output') before enqueue");
   hipStream_t st = (hipStream_t)stream;
   HIP_OR(hipSetDevice(c->e->device), "hipSetDevice");
-  const float* in = (const float*)c->in;
+  const void* in = c->in;
   float* out = (float*)c->out;
   if (c->prof_cb) {
     c->prof_used = 0;
@@ -998,6 +1023,22 @@ int mde_rt_event_elapsed_ms(float* ms, void* a, void* b) {
     if (e_ != hipSuccess) return hip_fail(e_, what);          \
     return MDE_OK;                                           \
   } while (0)
+
+int mde_op_patch_prep_u8(const unsigned char* img, int batch, int h, int w, float scale, const float* mean3,
+                         const float* std3, void* patches, void* st) {
+  if (!img || !mean3 || !std3 || !patches || batch < 1 || h % 14 || w % 14 || h < 14 || w < 14)
+    return fail(MDE_ERR_ARG, "mde_op_patch_prep_u8: bad argument (h, w multiples of 14)");
+  OP_RET(launch_patch_prep_u8(img, (h16*)patches, nullptr, nullptr, batch, h, w, h / 14, w / 14, 1, 0, scale, mean3,
+                              std3, (hipStream_t)st),
+         "patch_prep_u8");
+}
+
+int mde_op_depth_postprocess(const float* depth, int batch, int ih, int iw, float* out, int oh, int ow, float lo,
+                             float hi, void* st) {
+  if (!depth || !out || batch < 1 || ih < 1 || iw < 1 || oh < 1 || ow < 1)
+    return fail(MDE_ERR_ARG, "mde_op_depth_postprocess: bad argument");
+  OP_RET(launch_depth_postprocess(depth, batch, ih, iw, out, oh, ow, lo, hi, (hipStream_t)st), "depth_postprocess");
+}
 
 int mde_op_layernorm(const float* x, void* y, const float* g, const float* b, int rows, int dim, float eps,
                      int tokens, int skip_cls, void* st) {

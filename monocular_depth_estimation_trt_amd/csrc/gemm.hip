@@ -285,8 +285,8 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) 
   }
   float usy = 0.f, usx = 0.f;
   if constexpr (AM == A_CONV3_UP) {
-    usy = p.uh > 1 ? (float)(p.ch - 1) / (float)(p.uh - 1) : 0.f;
-    usx = p.uw > 1 ? (float)(p.cw - 1) / (float)(p.uw - 1) : 0.f;
+    usy = ac_scale(p.ch, p.uh);
+    usx = ac_scale(p.cw, p.uw);
   }
 
   // ---- B operand (weights [Npad][ldw], ldw % 64 == 0) ----
@@ -326,11 +326,10 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) 
         f16x8 v = zero8();
         const int iy = uy0[i] + ky, ix = ux0[i] + kx;
         if (uv[i] && kv && iy >= 0 && iy < p.uh && ix >= 0 && ix < p.uw) {
-          const float fy = usy * (float)iy, fx = usx * (float)ix;
-          const int y0 = (int)fy, x0 = (int)fx;
-          const int y1 = y0 + (y0 < p.ch - 1 ? 1 : 0), x1 = x0 + (x0 < p.cw - 1 ? 1 : 0);
-          const float ly1 = fy - (float)y0, ly0 = 1.f - ly1;
-          const float lx1 = fx - (float)x0, lx0 = 1.f - lx1;
+          int y0, y1, x0, x1;
+          float ly0, ly1, lx0, lx1;
+          ac_index(usy, iy, p.ch, y0, y1, ly0, ly1);
+          ac_index(usx, ix, p.cw, x0, x1, lx0, lx1);
           const f16* base = urow[i] + c0;
           const f16x8 a = *reinterpret_cast<const f16x8*>(base + ((size_t)y0 * p.cw + x0) * p.cc);
           const f16x8 b = *reinterpret_cast<const f16x8*>(base + ((size_t)y0 * p.cw + x1) * p.cc);

@@ -37,6 +37,25 @@ MDE_DEV float gelu_erf(float x) {
   return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(z));
 }
 
+// PyTorch upsample_bilinear2d(align_corners=True) source index and weights
+// (area_pixel_compute_scale / _source_index in fp32, then floor, clamp of the
+// +1 neighbour, lambda = src - i0), each op rounded as on the CPU: contraction
+// off, or the lambda would be taken from the unrounded product (errors up to
+// 5e-4 relative on steep maps).
+MDE_DEV float ac_scale(int in_size, int out_size) {
+#pragma clang fp contract(off)
+  return out_size > 1 ? (float)(in_size - 1) / (float)(out_size - 1) : 0.f;
+}
+
+MDE_DEV void ac_index(float scale, int dst, int in_size, int& i0, int& i1, float& l0, float& l1) {
+#pragma clang fp contract(off)
+  const float f = scale * (float)dst;
+  i0 = (int)f;
+  i1 = i0 + (i0 < in_size - 1 ? 1 : 0);
+  l1 = f - (float)i0;
+  l0 = 1.f - l1;
+}
+
 // Storage position of key t in a V^T row: inside every 32-key group the keys
 // are ordered [4 keys of sub-tile 0 | 4 keys of sub-tile 1] per 4-key lane
 // slot, so the 8 keys one MFMA lane consumes in P.V ({32g+4h+0..3,

@@ -78,6 +78,11 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
 hipError_t launch_layernorm(const float* x, h16* y, const float* g, const float* b, int rows, int D,
                             float eps, int T, int skip_cls, hipStream_t st);
 
+hipError_t launch_patch_prep_u8(const unsigned char* img, h16* P, float* X, const float* cls_pos, int B, int H, int W,
+                                int ph, int pw, int T, int D, float scale, const float* mean3, const float* std3,
+                                hipStream_t st);
+hipError_t launch_depth_postprocess(const float* in, int B, int ih, int iw, float* out, int oh, int ow, float lo,
+                                    float hi, hipStream_t st);
 hipError_t launch_patch_prep(const float* img, h16* P, float* X, const float* cls_pos, int B, int H,
                              int W, int ph, int pw, int T, int D, hipStream_t st);
 

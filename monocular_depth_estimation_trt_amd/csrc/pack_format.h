@@ -29,7 +29,12 @@ struct PackConfig {
   int32_t head_hidden, metric;
   float max_depth, ln_eps;
   char encoder[16];
-  char reserved[160];
+  // input preamble (reference core/onnx_tools.py:87-219 add_uint8_input):
+  // input_u8 = 1 -> the binding is "image_u8" uint8 NHWC [B,H,W,3] and the
+  // engine computes ((float)u / in_scale - in_mean[c]) / in_std[c] in fp32
+  int32_t input_u8;
+  float in_scale, in_mean[3], in_std[3];
+  char reserved[128];
 };
 static_assert(sizeof(PackConfig) == 256, "PackConfig");
 

@@ -26,10 +26,11 @@ class DataType(enum.IntEnum):
     """Subset of tensorrt.DataType (same values)."""
     FLOAT = 0
     HALF = 1
+    UINT8 = 5
 
     @property
     def itemsize(self) -> int:
-        return 4 if self == DataType.FLOAT else 2
+        return {DataType.FLOAT: 4, DataType.HALF: 2, DataType.UINT8: 1}[self]
 
 
 class TensorIOMode(enum.IntEnum):
@@ -40,7 +41,7 @@ class TensorIOMode(enum.IntEnum):
 
 def nptype(dt: DataType):
     """tensorrt.nptype analogue."""
-    return {DataType.FLOAT: np.float32, DataType.HALF: np.float16}[DataType(dt)]
+    return {DataType.FLOAT: np.float32, DataType.HALF: np.float16, DataType.UINT8: np.uint8}[DataType(dt)]
 
 
 def volume(shape: Sequence[int]) -> int:
@@ -148,6 +149,15 @@ class Engine:
     def input_hw(self) -> Tuple[int, int]:
         return int(self.info.img_h), int(self.info.img_w)
 
+    @property
+    def input_name(self) -> str:
+        """"input" (float32 NCHW) or "image_u8" (uint8 NHWC engines)."""
+        return next(r[0] for r in self._io if r[2])
+
+    @property
+    def input_format(self) -> str:
+        return "uint8_nhwc" if int(self.info.input_format) == 1 else "float32_nchw"
+
     def create_execution_context(self) -> "ExecutionContext":
         return ExecutionContext(self)
 
@@ -184,9 +194,9 @@ class ExecutionContext:
         engine._contexts.add(self)
         self._profiler = None
         self._cb = None
-        hw = engine.input_hw
         if not engine._profile:
-            self.set_input_shape("input", (engine._static_batch, 3, hw[0], hw[1]))
+            name = engine.input_name
+            self.set_input_shape(name, (engine._static_batch,) + tuple(engine._find(name)[3][1:]))
 
     @property
     def handle(self) -> C.c_void_p:

@@ -8,10 +8,15 @@
 
     python -m monocular_depth_estimation_trt_amd.models.depth_anything_v2.run \
         [--source synthetic:vits:metric | ckpt.pth] [--input x.npy] [--src-hw H W]
+        [--input-format float32_nchw | uint8_nhwc] [--host-postprocess]
 
 `--input` is an already-preprocessed float32 NCHW [1,3,518,518] tensor (the
-reference's core/preprocess.py needs cv2, absent here); without it a
-synthetic image of the spec's input domain is used.
+reference's core/preprocess.py needs cv2, absent here), or for
+`--input-format uint8_nhwc` the uint8 [1,518,518,3] image the reference's
+uint8 engine takes (core/onnx_tools.py:87-219: normalisation on the device);
+without it a synthetic image of the spec's input domain is used.  The
+post-process runs on the device (postprocess.DevicePostprocess) unless
+`--host-postprocess` asks for the reference's torch-CPU version.
 """
 
 import argparse
@@ -20,6 +25,7 @@ import os
 import numpy as np
 
 from monocular_depth_estimation_trt_amd import bench, common, spec, weights
+from monocular_depth_estimation_trt_amd.postprocess import DevicePostprocess
 from monocular_depth_estimation_trt_amd.common_runtime import allocate_buffers, do_inference, free_buffers
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -43,24 +49,39 @@ def main(argv=None):
     ap.add_argument("--iterations", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--out-dir", default=os.path.join(os.getcwd(), "reports", "bench"))
+    ap.add_argument("--input-format", choices=("float32_nchw", "uint8_nhwc"), default="float32_nchw")
+    ap.add_argument("--host-postprocess", action="store_true")
     a = ap.parse_args(argv)
+    u8 = a.input_format == "uint8_nhwc"
+    if u8 and a.engine.endswith("_fp16.mdeng"):
+        a.engine = a.engine[:-len("_fp16.mdeng")] + "_u8_fp16.mdeng"
 
     s = spec.load("depth_anything_v2")
     mc = spec.model_config_of(s)
     input_h, input_w = mc["input_hw"]
-    x = (np.load(a.input, allow_pickle=False).astype(np.float32) if a.input
-         else weights.synthetic_images(1, input_h, input_w, first_seed=0))
+    if u8:
+        x = (np.load(a.input, allow_pickle=False).astype(np.uint8) if a.input
+             else weights.synthetic_images_u8(1, input_h, input_w, first_seed=0))
+    else:
+        x = (np.load(a.input, allow_pickle=False).astype(np.float32) if a.input
+             else weights.synthetic_images(1, input_h, input_w, first_seed=0))
     output_shape = (1, input_h, input_w)
     with common.get_engine(a.source, a.engine, "fp16", None, encoder=mc["encoder"], depth_type=mc["depth_type"],
-                           max_depth=mc["max_depth"], input_hw=(input_h, input_w)) as engine, \
+                           max_depth=mc["max_depth"], input_hw=(input_h, input_w),
+                           input_format=a.input_format) as engine, \
             engine.create_execution_context() as context:
         inputs, outputs, bindings, stream = allocate_buffers(engine, output_shape, profile_idx=0)
         inputs[0].host = x
         outs, samples = bench.measure(
             lambda: do_inference(context, engine=engine, bindings=bindings, inputs=inputs, outputs=outputs,
                                  stream=stream), warmup=a.warmup, iterations=a.iterations)
-        depth = postprocess(outs[0].reshape(output_shape), a.src_hw)
+        if a.host_postprocess:
+            depth = postprocess(outs[0].reshape(output_shape), a.src_hw)
+        else:  # the engine's output is still in outputs[0].device
+            with DevicePostprocess(1, input_h, input_w, *a.src_hw) as pp:
+                depth = pp.run(outputs[0].device, stream)[0].copy()
         bench.record("depth_anything_v2", samples, warmup=a.warmup, precision="fp16", profile="bench",
+                     variant="u8" if u8 else "single",
                      input_h=input_h, input_w=input_w, engine_path=a.engine, outputs={"depth": depth},
                      encoder=mc["encoder"], notes=f"source={a.source}", model_input=x, out_dir=a.out_dir)
         print(f"[MDET] max : {depth.max():0.5f} , min : {depth.min():0.5f}")

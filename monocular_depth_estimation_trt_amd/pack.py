@@ -173,17 +173,36 @@ def packed_tensors(sd: Dict[str, np.ndarray], cfg: dict, img_h: int, img_w: int)
     return o
 
 
-def _config_bytes(cfg: dict, img_h: int, img_w: int) -> bytes:
+INPUT_FORMATS = ("float32_nchw", "uint8_nhwc")
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def _config_bytes(cfg: dict, img_h: int, img_w: int, input_format: str = "float32_nchw",
+                  mean=IMAGENET_MEAN, std=IMAGENET_STD, scale: float = 255.0) -> bytes:
+    """PackConfig (csrc/pack_format.h).  input_format "uint8_nhwc" stores the
+    preamble constants of the reference's add_uint8_input
+    (core/onnx_tools.py:87-219): ((u8 / scale) - mean) / std, fp32."""
+    if input_format not in INPUT_FORMATS:
+        raise ValueError(f"input_format must be one of {INPUT_FORMATS}, got {input_format!r}")
     oc, taps = cfg["out_channels"], cfg["taps"]
     b = struct.pack("<8i4i4i2i2f16s", cfg["embed_dim"], cfg["depth"], cfg["num_heads"], cfg["mlp_hidden"],
                     cfg["patch"], img_h, img_w, cfg["features"], *oc, *taps, cfg["head_hidden"],
                     1 if cfg["depth_type"] == "metric" else 0, float(cfg["max_depth"]), float(cfg["ln_eps"]),
                     cfg["encoder"].encode()[:15])
     assert len(b) == 96, len(b)
-    return b + b"\0" * 160
+    u8 = input_format == "uint8_nhwc"
+    if u8 and (len(mean) != 3 or len(std) != 3 or float(scale) == 0.0 or any(float(v) == 0.0 for v in std)):
+        raise ValueError("uint8 preamble needs 3 means, 3 non-zero stds and a non-zero scale")
+    b += struct.pack("<if3f3f", 1 if u8 else 0, float(scale) if u8 else 0.0,
+                     *([float(v) for v in mean] if u8 else [0.0] * 3),
+                     *([float(v) for v in std] if u8 else [0.0] * 3))
+    assert len(b) == 128, len(b)
+    return b + b"\0" * 128
 
 
-def pack_bytes(sd: Dict[str, np.ndarray], cfg: dict, img_h: int = 518, img_w: int = 518) -> bytes:
+def pack_bytes(sd: Dict[str, np.ndarray], cfg: dict, img_h: int = 518, img_w: int = 518,
+               input_format: str = "float32_nchw") -> bytes:
     tens = packed_tensors(sd, cfg, img_h, img_w)
     n = len(tens)
     table = bytearray()
@@ -202,7 +221,7 @@ def pack_bytes(sd: Dict[str, np.ndarray], cfg: dict, img_h: int = 518, img_w: in
     head_len = 32 + 256 + len(table)
     data_offset = -(-head_len // ALIGN) * ALIGN
     header = struct.pack("<8sIIQQ", b"MDEPACK1", PACK_VERSION, n, data_offset, len(data))
-    blob = header + _config_bytes(cfg, img_h, img_w) + bytes(table)
+    blob = header + _config_bytes(cfg, img_h, img_w, input_format) + bytes(table)
     blob += b"\0" * (data_offset - len(blob))
     return blob + bytes(data)
 
@@ -217,10 +236,10 @@ def write_packed(path: str, blob: bytes) -> str:
 
 
 def synthetic_blob(encoder: str = "vits", depth_type: str = "metric", img_h: int = 518, img_w: int = 518,
-                   seed: int = 1234) -> Tuple[bytes, dict]:
+                   seed: int = 1234, input_format: str = "float32_nchw") -> Tuple[bytes, dict]:
     cfg = W.model_config(encoder, depth_type)
     sd = W.synthetic_state_dict(cfg, seed)
-    return pack_bytes(sd, cfg, img_h, img_w), cfg
+    return pack_bytes(sd, cfg, img_h, img_w, input_format), cfg
 
 
 def fingerprint(blob: bytes, arch: str = "gfx950") -> str:

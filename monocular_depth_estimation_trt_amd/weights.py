@@ -152,6 +152,16 @@ IMAGENET_MEAN = np.array([0.485, 0.456, 0.406], np.float64)
 IMAGENET_STD = np.array([0.229, 0.224, 0.225], np.float64)
 
 
+def synthetic_images_u8(batch: int, h: int = 518, w: int = 518, first_seed: int = 0) -> np.ndarray:
+    """The same pixels as synthetic_images() before normalisation: uint8 NHWC
+    [batch, h, w, 3] (the "image_u8" binding of a uint8_nhwc engine)."""
+    out = np.empty((batch, h, w, 3), np.uint8)
+    for i in range(batch):
+        rng = np.random.Generator(np.random.PCG64(first_seed + i))
+        out[i] = rng.integers(0, 256, size=(h, w, 3), dtype=np.uint8)
+    return out
+
+
 def synthetic_images(batch: int, h: int = 518, w: int = 518, first_seed: int = 0) -> np.ndarray:
     """The benchmark input domain: u ~ U{0..255} per pixel (PCG64 seed i for
     image i), then (u/255 - mean)/std in float64 -> float32 NCHW.  This is the

@@ -44,7 +44,18 @@ def test_python_binding_covers_the_header(lib_path):
     assert set(declared_functions()) == set(_lib.PROTOTYPES), \
         set(declared_functions()) ^ set(_lib.PROTOTYPES)
     L = _lib.lib()
-    assert L.mde_version() == 1
+    ver = int(re.search(r"#define MDE_ABI_VERSION (\d+)", open(HEADER).read()).group(1))
+    assert L.mde_version() == ver
+
+
+def test_info_struct_matches_header():
+    """ctypes mirror of mde_engine_info / mde_io_desc has every header field, in order."""
+    from monocular_depth_estimation_trt_amd import _lib
+    txt = open(HEADER).read()
+    body = re.search(r"typedef struct \{([^}]*)\} mde_engine_info;", txt).group(1)
+    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
+    names = re.findall(r"([a-z_0-9]+)(?:\[\d+\])?\s*[,;]", body)
+    assert names == [f[0] for f in _lib.mde_engine_info._fields_]
 
 
 def test_errors_without_gpu_are_reported_not_crashed(lib_path):
