@@ -42,6 +42,7 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 MFMA_PEAK_TFLOPS = 2500.0   # dense fp16/bf16 MFMA, MI355X (MI355X_MICROARCH.md chip table)
+ENC_LABEL = {"vits": "ViT-S", "vitb": "ViT-B", "vitl": "ViT-L"}
 REF_B1_FPS = 232.11         # RTX 3080 TRT fp16, BASELINE.md
 REF_B1_U8_FPS = 294.07      # same, uint8-NHWC input engine (reports/uint8_ab/depth_anything_v2.json)
 
@@ -239,7 +240,7 @@ def main():
     for c, v in list(breakdown.items())[:8]:
         log(f"{c:24s} {v['ms']:9.4f} ms  x{v['launches']:3d}  {v['tflops']} TF/s")
     line = {
-        "metric": "depth FPS (images/s) at 518x518 fp16, DA-V2 ViT-S, MI355X",
+        "metric": f"depth FPS (images/s) at {S}x{S} fp16, DA-V2 {ENC_LABEL.get(a.encoder, a.encoder)}, MI355X",
         "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": round(value / REF_B1_FPS, 3), "dtype": "fp16", "data": "synthetic",

@@ -1,5 +1,7 @@
-"""Depth Anything V2 on MI355X -- the counterpart of the reference driver
-`models/depth_anything_v2/onnx2trt.py:main` (:42-127), same sequence:
+"""Depth Anything V2 (and its family) on MI355X -- the counterpart of the
+reference drivers `models/depth_anything_v2/onnx2trt.py:main` (:42-127),
+`models/depth_anything_ac/onnx2trt.py` and `models/distill_any_depth/
+onnx2trt.py` (the same ViT-S DA-V2 graph, relative head), same sequence:
 
   input -> get_engine -> create_execution_context -> allocate_buffers ->
   bench.measure(do_inference) (20 warmup / 100 iterations) ->
@@ -40,10 +42,14 @@ def postprocess(depth: np.ndarray, src_hw) -> np.ndarray:
     return torch.clamp(t, min=1e-3, max=1e3).numpy()
 
 
-def main(argv=None):
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--source", default="synthetic:vits:metric:1234")
-    ap.add_argument("--engine", default=os.path.join(HERE, "engine", "depth_anything_v2_vits_518x518_fp16.mdeng"))
+def main(argv=None, model="depth_anything_v2"):
+    s = spec.load(model)
+    mc = spec.model_config_of(s)
+    input_h, input_w = mc["input_hw"]
+    ap = argparse.ArgumentParser(prog=model)
+    ap.add_argument("--source", default=f"synthetic:{mc['encoder']}:{mc['depth_type']}:1234")
+    ap.add_argument("--engine", default=os.path.join(os.path.dirname(HERE), model, "engine",
+                                                     f"{model}_{mc['encoder']}_{input_h}x{input_w}_fp16.mdeng"))
     ap.add_argument("--input", default="")
     ap.add_argument("--src-hw", type=int, nargs=2, default=[2268, 3024])
     ap.add_argument("--iterations", type=int, default=100)
@@ -55,10 +61,6 @@ def main(argv=None):
     u8 = a.input_format == "uint8_nhwc"
     if u8 and a.engine.endswith("_fp16.mdeng"):
         a.engine = a.engine[:-len("_fp16.mdeng")] + "_u8_fp16.mdeng"
-
-    s = spec.load("depth_anything_v2")
-    mc = spec.model_config_of(s)
-    input_h, input_w = mc["input_hw"]
     if u8:
         x = (np.load(a.input, allow_pickle=False).astype(np.uint8) if a.input
              else weights.synthetic_images_u8(1, input_h, input_w, first_seed=0))
@@ -75,12 +77,14 @@ def main(argv=None):
         outs, samples = bench.measure(
             lambda: do_inference(context, engine=engine, bindings=bindings, inputs=inputs, outputs=outputs,
                                  stream=stream), warmup=a.warmup, iterations=a.iterations)
-        if a.host_postprocess:
+        if mc["postprocess"] == "none":   # distill_any_depth: the 518x518 map as is (its onnx2trt.py:98-100)
+            depth = outs[0].reshape(output_shape)[0].copy()
+        elif a.host_postprocess:
             depth = postprocess(outs[0].reshape(output_shape), a.src_hw)
         else:  # the engine's output is still in outputs[0].device
             with DevicePostprocess(1, input_h, input_w, *a.src_hw) as pp:
                 depth = pp.run(outputs[0].device, stream)[0].copy()
-        bench.record("depth_anything_v2", samples, warmup=a.warmup, precision="fp16", profile="bench",
+        bench.record(model, samples, warmup=a.warmup, precision="fp16", profile="bench",
                      variant="u8" if u8 else "single",
                      input_h=input_h, input_w=input_w, engine_path=a.engine, outputs={"depth": depth},
                      encoder=mc["encoder"], notes=f"source={a.source}", model_input=x, out_dir=a.out_dir)

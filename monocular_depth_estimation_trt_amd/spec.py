@@ -86,9 +86,17 @@ def caveats(spec):
     return list(spec.get("caveats", []))
 
 
+# checkpoint-family encoder names -> DA-V2 encoder (distill_any_depth uses
+# small/base/large for the vits/vitb/vitl graphs, reference
+# models/distill_any_depth/infer.py:32-69)
+ENCODER_ALIASES = {"small": "vits", "base": "vitb", "large": "vitl"}
+
+
 def model_config_of(spec):
-    """The engine build config a DA-V2 spec implies (encoder, head, size)."""
+    """The engine build config a DA-V2-family spec implies (encoder, head,
+    size, post-process)."""
     enc = spec.get("encoder", {}).get("used", "vits")
+    enc = ENCODER_ALIASES.get(enc, enc)
     depth_type = "metric" if spec.get("depth_scale", "metric") == "metric" else "relative"
     return {"encoder": enc, "depth_type": depth_type, "max_depth": float(spec.get("max_depth", 20.0)),
-            "input_hw": size_of(spec)}
+            "input_hw": size_of(spec), "postprocess": spec.get("postprocess", "resize_clamp")}

@@ -13,6 +13,7 @@ run time is absent here, so HF is the executable stand-in.
 Fixtures written (small, npz, float32 unless noted):
   dav2_vits_metric_98.npz    B=2 98x98 ViT-S metric: input, HF output, digest
   dav2_vits_relative_98.npz  B=1 98x98 ViT-S relative head
+  dav2_vitb_relative_98.npz  B=1 98x98 ViT-B relative head (D=768, 12 heads, F=128)
   dav2_vitl_metric_98.npz    B=1 98x98 ViT-L metric (taps 4/11/17/23, F=256)
   dav2_vits_metric_518.npz   B=1 518x518 ViT-S metric: output subsampled
                              every 7th pixel + full-map stats
@@ -194,13 +195,24 @@ def pos_case():
     np.savez_compressed(os.path.join(HERE, "posembed_upstream.npz"), **rec)
 
 
+CASES = {
+    "dav2_vits_metric_98": ("vits", "metric", 2, 98, True),
+    "dav2_vits_relative_98": ("vits", "relative", 1, 98, True),
+    "dav2_vitb_relative_98": ("vitb", "relative", 1, 98, True),
+    "dav2_vitl_metric_98": ("vitl", "metric", 1, 98, True),
+    "dav2_vits_metric_518": ("vits", "metric", 1, 518, False),
+}
+
+
 def main():
+    """python tests/golden/make_golden.py [case ...]  (default: all + pos-embed)"""
     torch.set_num_threads(os.cpu_count() or 8)
-    pos_case()
-    run_case("dav2_vits_metric_98", "vits", "metric", 2, 98)
-    run_case("dav2_vits_relative_98", "vits", "relative", 1, 98)
-    run_case("dav2_vitl_metric_98", "vitl", "metric", 1, 98)
-    run_case("dav2_vits_metric_518", "vits", "metric", 1, 518, full=False)
+    only = sys.argv[1:]
+    if not only:
+        pos_case()
+    for name, (enc, dt, b, size, full) in CASES.items():
+        if not only or name in only:
+            run_case(name, enc, dt, b, size, full=full)
 
 
 if __name__ == "__main__":

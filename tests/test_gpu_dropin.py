@@ -95,3 +95,17 @@ def test_driver_script(gpu):
                       "--src-hw", "300", "400", "--out-dir", os.path.join(td, "bench")])
         assert d.shape == (300, 400) and np.isfinite(d).all() and d.min() >= 1e-3
         assert os.path.exists(os.path.join(td, "bench", "depth_anything_v2_518x518_bench_single_fp16.json"))
+
+
+@pytest.mark.parametrize("model", ["depth_anything_ac", "distill_any_depth"])
+def test_family_drivers(gpu, model):
+    """The DA-V2 family drivers (relative head) run the reference sequence;
+    distill_any_depth keeps the 518x518 map, depth_anything_ac resizes+clamps."""
+    import importlib
+    run = importlib.import_module(f"monocular_depth_estimation_trt_amd.models.{model}.run")
+    with tempfile.TemporaryDirectory() as td:
+        d = run.main(["--engine", os.path.join(td, "e_fp16.mdeng"), "--iterations", "2", "--warmup", "1",
+                      "--src-hw", "300", "400", "--out-dir", os.path.join(td, "bench")])
+        assert os.path.exists(os.path.join(td, "bench", f"{model}_518x518_bench_single_fp16.json"))
+    assert np.isfinite(d).all() and d.min() >= 0.0
+    assert d.shape == ((518, 518) if model == "distill_any_depth" else (300, 400))

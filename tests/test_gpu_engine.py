@@ -60,7 +60,7 @@ def check(y, ref, max_depth, what):
     return m
 
 
-@pytest.mark.parametrize("name", ["dav2_vits_metric_98", "dav2_vits_relative_98", "dav2_vitl_metric_98"])
+@pytest.mark.parametrize("name", ["dav2_vits_metric_98", "dav2_vits_relative_98", "dav2_vitb_relative_98", "dav2_vitl_metric_98"])
 def test_engine_vs_golden_98(gpu, name):
     z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     enc, dt = str(z["encoder"]), str(z["depth_type"])

@@ -18,7 +18,7 @@ def _load(name):
     return np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
 
 
-@pytest.mark.parametrize("name", ["dav2_vits_metric_98", "dav2_vits_relative_98", "dav2_vitl_metric_98"])
+@pytest.mark.parametrize("name", ["dav2_vits_metric_98", "dav2_vits_relative_98", "dav2_vitb_relative_98", "dav2_vitl_metric_98"])
 def test_oracle_matches_hf_golden(name):
     z = _load(name)
     cfg = weights.model_config(str(z["encoder"]), str(z["depth_type"]))

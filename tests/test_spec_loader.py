@@ -18,8 +18,26 @@ def test_shipped_spec():
     assert s["input"]["name"] == "input" and s["outputs"][0]["name"] == "output"
     assert s["build_targets"][0]["precision"] == "fp16"
     assert spec.model_config_of(s) == {"encoder": "vits", "depth_type": "metric", "max_depth": 20.0,
-                                       "input_hw": (518, 518)}
-    assert "depth_anything_v2" in spec.load_all()
+                                       "input_hw": (518, 518), "postprocess": "resize_clamp"}
+    assert {"depth_anything_v2", "depth_anything_ac", "distill_any_depth"} <= set(spec.load_all())
+
+
+@pytest.mark.parametrize("name,post", [("depth_anything_ac", "resize_clamp"), ("distill_any_depth", "none")])
+def test_family_specs(name, post):
+    """The DA-V2 family: the same ViT-S graph with the
+    relative head; distill_any_depth's 'small' is the vits graph."""
+    mc = spec.model_config_of(spec.load(name))
+    assert mc["encoder"] == "vits" and mc["depth_type"] == "relative" and mc["postprocess"] == post
+    assert mc["input_hw"] == (518, 518)
+
+
+@pytest.mark.parametrize("name", ["depth_anything_ac", "distill_any_depth"])
+def test_reference_family_specs_load_unchanged(name):
+    p = f"/root/reference/models/{name}/spec.json"
+    if not os.path.exists(p):
+        pytest.skip("reference checkout not present")
+    mc = spec.model_config_of(spec.load(p))
+    assert mc["encoder"] == "vits" and mc["depth_type"] == "relative"
 
 
 @pytest.mark.skipif(not os.path.exists(REF_SPEC), reason="reference checkout not present")
