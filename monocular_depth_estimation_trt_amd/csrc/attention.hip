@@ -38,6 +38,13 @@ constexpr int KT = 64;        // keys per tile
 constexpr int TILE_B = KT * 128;  // bytes of one K (or V^T) tile image: 64 rows x 128 B
 
 typedef f16 f16x4v __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// Deferred rescale (cdna_hip_programming.md 5.5 T13): the running max moves
+// only when a tile's max exceeds it by more than RESCALE_T (log2 units), so
+// p = exp2(S - m_run) <= 2^RESCALE_T = 256 -- exact in f16's range, and the
+// rescale branch (O, l *= 2^-delta) is taken a few times per row, not per tile.
+constexpr float RESCALE_T = 8.f;
 
 // byte offset of 16-B chunk `chunk` of a 128-B row: conflict-free ds_read_b128
 MDE_DEV int kswz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
@@ -143,8 +150,9 @@ __global__ void __launch_bounds__(NW * 64) attn_fwd_kernel(const f16* __restrict
   }
   lds_barrier();
 
-  auto tile = [&](int kt, int slot, auto first_tag) {
+  auto tile = [&](int kt, auto slot_tag, auto first_tag) {
     constexpr bool FIRST = decltype(first_tag)::value;
+    constexpr int slot = decltype(slot_tag)::value;  // compile-time: LDS offsets fold into ds_read immediates
     const char* K_ = smem + slot * SLOT;
     const char* V_ = K_ + TILE_B;
     // S'^T[key][query] = K Q^T - m_run: 4 key sub-tiles x NQ query blocks
@@ -173,12 +181,17 @@ __global__ void __launch_bounds__(NW * 64) attn_fwd_kernel(const f16* __restrict
     f16x8 pb[NQ][2];
 #pragma unroll
     for (int c = 0; c < NQ; ++c) {
-      float mx = fmaxf(fmaxf(fmaxf(s[c][0][0], s[c][0][1]), fmaxf(s[c][0][2], s[c][0][3])),
-                       fmaxf(fmaxf(s[c][1][0], s[c][1][1]), fmaxf(s[c][1][2], s[c][1][3])));
-      mx = fmaxf(mx, fmaxf(fmaxf(fmaxf(s[c][2][0], s[c][2][1]), fmaxf(s[c][2][2], s[c][2][3])),
-                           fmaxf(fmaxf(s[c][3][0], s[c][3][1]), fmaxf(s[c][3][2], s[c][3][3]))));
+      // max over the lane's 16 scores as a chain of v_max3 (8 ops)
+      float mx = fmaxf(fmaxf(s[c][0][0], s[c][0][1]), s[c][0][2]);
+      mx = fmaxf(fmaxf(mx, s[c][0][3]), s[c][1][0]);
+      mx = fmaxf(fmaxf(mx, s[c][1][1]), s[c][1][2]);
+      mx = fmaxf(fmaxf(mx, s[c][1][3]), s[c][2][0]);
+      mx = fmaxf(fmaxf(mx, s[c][2][1]), s[c][2][2]);
+      mx = fmaxf(fmaxf(mx, s[c][2][3]), s[c][3][0]);
+      mx = fmaxf(fmaxf(mx, s[c][3][1]), s[c][3][2]);
+      mx = fmaxf(mx, s[c][3][3]);
       mx = xmax4(mx);  // max of S' over the tile (relative to m_run)
-      if (FIRST || __any(mx > 0.f)) {
+      if (FIRST || __any(mx > RESCALE_T)) {
         // the running max grows by delta >= 0: shift S', rescale O and l
         const float delta = FIRST ? mx : fmaxf(mx, 0.f);
         m_run[c] += delta;
@@ -192,16 +205,17 @@ __global__ void __launch_bounds__(NW * 64) attn_fwd_kernel(const f16* __restrict
           for (int d = 0; d < 4; ++d) acc[c][d] *= alpha;
         }
       }
-      float ls = 0.f;
+      f32x2 ls2 = {0.f, 0.f};  // packed row sums (v_pk_add_f32)
 #pragma unroll
       for (int t4 = 0; t4 < 4; ++t4)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          const float pv = __builtin_amdgcn_exp2f(s[c][t4][r]);
-          s[c][t4][r] = pv;
-          ls += pv;
+        for (int r = 0; r < 4; r += 2) {
+          const f32x2 pv = {__builtin_amdgcn_exp2f(s[c][t4][r]), __builtin_amdgcn_exp2f(s[c][t4][r + 1])};
+          s[c][t4][r] = pv[0];
+          s[c][t4][r + 1] = pv[1];
+          ls2 += pv;
         }
-      l_run[c] += ls;
+      l_run[c] += ls2[0] + ls2[1];
       // P^T as B operand: k index j<4 -> key sub-tile 2ks, j>=4 -> 2ks+1 (rows 4hq+r)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
@@ -225,18 +239,30 @@ __global__ void __launch_bounds__(NW * 64) attn_fwd_kernel(const f16* __restrict
     }
   };
 
-  int slot = 0;
-  for (int kt = 0; kt < nkt; ++kt) {
-    if (kt + 2 < nkt) issue(kt + 2, slot == 0 ? 2 : slot - 1);
-    if (kt == 0) tile(kt, slot, std::true_type{});
-    else tile(kt, slot, std::false_type{});
+  // tile kt lives in ring slot kt % 3; the loop is unrolled over the three
+  // slots so every LDS address is lane base + immediate
+  auto step = [&](int kt, auto slot_tag, auto first_tag) {
+    constexpr int SL = decltype(slot_tag)::value;
+    if (kt + 2 < nkt) issue(kt + 2, (SL + 2) % 3);
+    tile(kt, slot_tag, first_tag);
     // tile kt+1 must have landed before anyone reads it; its slot's previous
     // contents (tile kt-2) were released at the previous barrier
     if (kt + 2 < nkt) wait_vm_n<PER_TILE>();
     else wait_vm_n<0>();
     lds_barrier();
-    slot = slot == 2 ? 0 : slot + 1;
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  using S2 = std::integral_constant<int, 2>;
+  step(0, S0{}, std::true_type{});
+  int kt = 1;
+  for (; kt + 3 <= nkt; kt += 3) {
+    step(kt, S1{}, std::false_type{});
+    step(kt + 1, S2{}, std::false_type{});
+    step(kt + 2, S0{}, std::false_type{});
   }
+  if (kt < nkt) step(kt++, S1{}, std::false_type{});
+  if (kt < nkt) step(kt++, S2{}, std::false_type{});
 
 #pragma unroll
   for (int c = 0; c < NQ; ++c) {
