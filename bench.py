@@ -89,6 +89,31 @@ def profile_layers(ctx, stream, iters):
     return {k: statistics.median(v) for k, v in prof.ms.items()}
 
 
+# layer class -> kernel symbol substring in rocprofv3 traces (classes whose
+# launches map to one kernel template; GEMM classes share gemm_kernel<...>)
+CLASS_KERNEL = {"attn": "attn_fwd_kernel"}
+
+
+def pmc_traffic(cls, cfg, B, size):
+    """HBM bytes per launch of the dominant class's kernel from the committed
+    PMC profile of this workload (tools/profile_round.sh -> profiles/
+    traffic_<enc>_b<B>.json: FETCH_SIZE x2 + WRITE_SIZE, separate passes), or
+    None.  Attention is matched by kernel name and grid size."""
+    path = os.path.join(ROOT, "profiles", f"traffic_{cfg['encoder']}_b{B}_{size}.json")
+    sub = CLASS_KERNEL.get(cls)
+    if not sub or not os.path.exists(path):
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    grid = None
+    if cls == "attn":
+        grid = ((1370 if size == 518 else (size // 14) ** 2 + 1) + 127) // 128 * B * cfg["num_heads"] * 512
+    for r in d["kernels"]:
+        if sub in r["kernel"] and (grid is None or r["grid"] == grid):
+            return r["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def roofline(cfg, B, size, layer_ms):
     from monocular_depth_estimation_trt_amd import flops
     lf = flops.layer_flops(cfg, size, size, B)
@@ -105,10 +130,15 @@ def roofline(cfg, B, size, layer_ms):
     breakdown = {c: {"ms": round(cls_ms[c], 4), "launches": cls_n[c],
                      "tflops": round(cls_fl[c] / (cls_ms[c] * 1e-3) / 1e12, 1) if cls_fl.get(c) else None}
                  for c in sorted(cls_ms, key=lambda c: -cls_ms[c])}
-    return {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": MFMA_PEAK_TFLOPS,
-            "unit": "TFLOP/s", "frac": round(achieved / MFMA_PEAK_TFLOPS, 4), "traffic": None,
+    traffic, src = pmc_traffic(dom, cfg, B, size)
+    roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": MFMA_PEAK_TFLOPS,
+            "unit": "TFLOP/s", "frac": round(achieved / MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
             "flop_per_launch": per_launch_fl, "avg_launch_ms": round(avg_ms, 5),
-            "launches_per_step": cls_n[dom]}, breakdown
+            "launches_per_step": cls_n[dom]}
+    if traffic is not None:
+        roof["traffic_unit"] = "bytes/launch"
+        roof["traffic_source"] = src
+    return roof, breakdown
 
 
 def b1_reference_method(blob, dev, size, warmup, iters, u8=False, prefix="b1_"):
