@@ -132,8 +132,13 @@ int load_pack(const uint8_t* data, size_t n, int device, mde_engine** out) {
       c.img_h <= 0 || c.img_w <= 0 || c.features % 16 || c.head_hidden != 32) {
     delete e;
     return fail(MDE_ERR_FORMAT, "unsupported model geometry in packed config");
-  if (c.input_u8 != 0 && c.input_u8 != 1) return fail(MDE_ERR_FORMAT, "bad input format in packed config");
-  if (c.input_u8 && (c.in_scale == 0.f || c.in_std[0] == 0.f || c.in_std[1] == 0.f || c.in_std[2] == 0.f))
+  }
+  if (c.input_u8 != 0 && c.input_u8 != 1) {
+    delete e;
+    return fail(MDE_ERR_FORMAT, "bad input format in packed config");
+  }
+  if (c.input_u8 && (c.in_scale == 0.f || c.in_std[0] == 0.f || c.in_std[1] == 0.f || c.in_std[2] == 0.f)) {
+    delete e;
     return fail(MDE_ERR_FORMAT, "uint8 input preamble with a zero scale/std");
   }
   hipError_t he = hipSetDevice(device);
