@@ -1,6 +1,6 @@
 /*
- * mde.h -- C ABI of libmde_hip.so, the MI355X (gfx950) Depth Anything V2
- * inference engine.  Plain pointers, sizes and ints only: no torch, no HIP
+ * mde.h -- C ABI of libmde_hip.so, the MI355X (gfx950) monocular depth
+ * inference engine (Depth Anything V2 family; Depth Pro).  Plain pointers, sizes and ints only: no torch, no HIP
  * C++ types (streams/events are opaque `void*` = hipStream_t / hipEvent_t).
  *
  * Every function returns 0 (MDE_OK) on success or an mde_status code;
@@ -13,6 +13,8 @@
  *                 (deserialize_cuda_engine, :298-299) and its introspection
  *                 used by core/common_runtime.py:131-175 (num_io_tensors,
  *                 get_tensor_name/shape/dtype/mode, get_tensor_profile_shape)
+ *                 Depth Pro: models/depth_pro/onnx2trt.py:94-111 (same engine API,
+ *                 outputs "canonical_inverse_depth" + "fov_deg", onnx_export.py:56)
  *   context       engine.create_execution_context()
  *                 (models/depth_anything_v2/onnx2trt.py:93-94),
  *                 context.set_tensor_address (core/common_runtime.py:272-274),
@@ -38,7 +40,7 @@
 extern "C" {
 #endif
 
-#define MDE_ABI_VERSION 2
+#define MDE_ABI_VERSION 3
 
 typedef enum {
   MDE_OK = 0,
@@ -74,6 +76,9 @@ typedef struct {
   int32_t max_batch_hint;
   int64_t weight_bytes;
   int32_t input_format; /* 0: "input" float32 NCHW [B,3,H,W]; 1: "image_u8" uint8 NHWC [B,H,W,3] */
+  int32_t family;       /* 0: Depth Anything V2 (io "input" -> "output" [B,H,W]);
+                           1: Depth Pro (io "input" [B,3,1536,1536] -> "canonical_inverse_depth"
+                              [B,1,1536,1536] and, with the FOV head, "fov_deg" [B]) */
 } mde_engine_info;
 
 /* IProfiler.report_layer_time analogue: one call per launched layer. */
@@ -173,6 +178,18 @@ int mde_op_patch_prep_u8(const unsigned char* img_u8, int batch, int h, int w, f
  * align_corners=True resize of fp32 depth [batch][ih][iw] to [batch][oh][ow], then clamp to [lo, hi]. */
 int mde_op_depth_postprocess(const float* depth, int batch, int ih, int iw, float* out, int oh, int ow, float lo,
                              float hi, void* stream);
+/* Depth Pro pyramid patches (upstream DepthProEncoder._create_pyramid + _split, reference engine input
+ * "input"): fp32 NCHW image [batch][3][size][size] (size = 4 * 384) -> f16 patch-embed rows
+ * [nseq * batch * 576][768] ((c, py, px) order), sequence s = patch * batch + image with the 25
+ * x1 patches (stride 288) first, then the 9 x0.5 patches (stride 192), then the x0.25 image;
+ * downsampling = bilinear, align_corners=False, computed on the fly. */
+int mde_op_dp_pyramid_patches(const float* img, int batch, int size, void* patches_f16, void* stream);
+/* Merge encoder rows x32 [.. sequences][tokens][dim] (row 0 of each sequence = cls, dropped) of
+ * the n x n patches (base + r*n + c) * batch + b into an NHWC f16 map [batch][side][side][dim],
+ * side = n*g - 2(n-1)*pad, trimming `pad` rows/cols on interior patch edges (upstream _merge);
+ * gamma/beta non-null: LayerNorm(eps) fused into the gather, else a plain fp32 -> f16 copy. */
+int mde_op_merge_tokens(const float* x32, int batch, int tokens, int dim, int n, int g, int pad, int base,
+                        const float* gamma, const float* beta, float eps, void* out_f16, void* stream);
 
 #ifdef __cplusplus
 }

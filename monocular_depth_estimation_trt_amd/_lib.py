@@ -38,7 +38,7 @@ class mde_engine_info(C.Structure):
                 ("out_channels", C.c_int32 * 4), ("taps", C.c_int32 * 4),
                 ("max_depth", C.c_float), ("ln_eps", C.c_float),
                 ("max_batch_hint", C.c_int32), ("weight_bytes", C.c_int64),
-                ("input_format", C.c_int32)]
+                ("input_format", C.c_int32), ("family", C.c_int32)]
 
 
 LAYER_CB = C.CFUNCTYPE(None, c_char_p, c_float, c_void_p)
@@ -102,6 +102,9 @@ PROTOTYPES = {
     "mde_op_depth_head": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p,
                           c_void_p, c_float, c_int, c_float, c_void_p, c_void_p],
     "mde_op_patch_prep_u8": [c_void_p, c_int, c_int, c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
+    "mde_op_dp_pyramid_patches": [c_void_p, c_int, c_int, c_void_p, c_void_p],
+    "mde_op_merge_tokens": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float,
+                            c_void_p, c_void_p],
     "mde_op_depth_postprocess": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_float, c_float,
                                  c_void_p],
 }

@@ -10,7 +10,8 @@ same reuse/rebuild rules, same errors (FileNotFoundError for a missing
 source, RuntimeError for a failed build/load).
 
 Source strings:
-  synthetic:<vits|vitb|vitl>[:<metric|relative>[:<seed>]]   seeded weights
+  synthetic:<vits|vitb|vitl>[:<metric|relative>[:<seed>]]   seeded DA-V2 weights
+  synthetic:depth_pro[:<dinov2l16_384|tiny>[:<seed>]]       seeded Depth Pro weights
   /path/ckpt.pth          torch.load(..., weights_only=True)
   /path/ckpt.safetensors  safetensors
   /path/ckpt.npz          numpy (allow_pickle=False)
@@ -25,7 +26,7 @@ from typing import Optional, Sequence
 
 import numpy as np
 
-from . import pack, weights
+from . import pack, pack_depth_pro, weights, weights_depth_pro
 from .common_runtime import *  # noqa: F401,F403  (re-export, as core/common.py does)
 from .engine import Engine
 
@@ -69,6 +70,25 @@ def load_checkpoint(path: str) -> dict:
     if isinstance(sd, dict) and "model" in sd and isinstance(sd["model"], dict):
         sd = sd["model"]
     return {k: v.float().numpy() for k, v in sd.items()}
+
+
+def is_depth_pro_source(src: str, sd: Optional[dict] = None) -> bool:
+    """Depth Pro sources: synthetic:depth_pro[...] or an HF-keyed Depth Pro state dict."""
+    if src.startswith("synthetic:"):
+        return src.split(":")[1] == "depth_pro"
+    return sd is not None and any(k.startswith("depth_pro.encoder.") for k in sd)
+
+
+def _depth_pro_config_of(sd: dict) -> dict:
+    """The Depth Pro preset a checkpoint matches (by ViT width / depth and the FOV head)."""
+    D = np.asarray(sd["depth_pro.encoder.patch_encoder.model.embeddings.cls_token"]).shape[-1]
+    use_fov = any(k.startswith("fov_model.") for k in sd)
+    for preset, v in weights_depth_pro.VIT.items():
+        cfg = weights_depth_pro.depth_pro_config(preset, use_fov=use_fov)
+        if v["embed_dim"] == D and all(k in sd for k in weights_depth_pro.expected_keys(cfg)
+                                       if not k.endswith("mask_token")):
+            return cfg
+    raise ValueError(f"no Depth Pro preset matches this checkpoint (embed dim {D})")
 
 
 def _infer_encoder(sd: dict) -> str:
@@ -168,11 +188,19 @@ def get_engine(onnx_file_path, engine_file_path="", precision="fp32", dynamic_in
         nonlocal sd, encoder
         if not present:
             raise FileNotFoundError(f"[MDET] source {src} not found.")
+        if is_depth_pro_source(src):
+            parts = src.split(":")
+            cfg = weights_depth_pro.depth_pro_config(parts[2] if len(parts) > 2 and parts[2] else "dinov2l16_384")
+            sd = weights_depth_pro.synthetic_state_dict(cfg, int(parts[3]) if len(parts) > 3 and parts[3] else 4321)
+            return pack_depth_pro.pack_bytes(sd, cfg)
+        if not src.startswith("synthetic:"):
+            sd = load_checkpoint(src)
+            if is_depth_pro_source(src, sd):
+                return pack_depth_pro.pack_bytes(sd, _depth_pro_config_of(sd))
         if src.startswith("synthetic:"):
             cfg = weights.model_config(encoder, depth_type, max_depth)
             sd = weights.synthetic_state_dict(cfg, _parse_synthetic(src)[2])
         else:
-            sd = load_checkpoint(src)
             encoder = encoder or _infer_encoder(sd)
             cfg = weights.model_config(encoder, depth_type, max_depth)
         return pack.pack_bytes(sd, cfg, *input_hw, input_format=input_format)

@@ -238,8 +238,9 @@ hipError_t launch_conv3(const GemmParams& p, hipStream_t st) {
   const bool up = p.amode == A_CONV3_UP;
   const bool ck64 = (p.cc % 64) == 0 && p.stride == 1;
   if (p.emode == E_HEAD) {
-    if (p.N != 32 || !up) return hipErrorInvalidValue;
-    return ck64 ? conv_tiles<64, 1, true, E_HEAD>(p, st) : conv_tiles<32, 1, true, E_HEAD>(p, st);
+    if (p.N != 32 || p.stride != 1) return hipErrorInvalidValue;
+    if (up) return ck64 ? conv_tiles<64, 1, true, E_HEAD>(p, st) : conv_tiles<32, 1, true, E_HEAD>(p, st);
+    return ck64 ? conv_tiles<64, 1, false, E_HEAD>(p, st) : conv_tiles<32, 1, false, E_HEAD>(p, st);
   }
   if (p.emode != E_STORE) return hipErrorInvalidValue;
   if (up) return ck64 ? conv_tiles<64, 1, true, E_STORE>(p, st) : conv_tiles<32, 1, true, E_STORE>(p, st);

@@ -191,6 +191,8 @@ hipError_t launch_layernorm(const float* x, h16* y, const float* g, const float*
   dim3 grid((rows + 3) / 4), block(256);
   f16* yo = reinterpret_cast<f16*>(y);
   switch (D) {
+    case 128: hipLaunchKernelGGL(layernorm_kernel<2>, grid, block, 0, st, x, yo, g, b, rows, eps, T, skip_cls); break;
+    case 256: hipLaunchKernelGGL(layernorm_kernel<4>, grid, block, 0, st, x, yo, g, b, rows, eps, T, skip_cls); break;
     case 384: hipLaunchKernelGGL(layernorm_kernel<6>, grid, block, 0, st, x, yo, g, b, rows, eps, T, skip_cls); break;
     case 768: hipLaunchKernelGGL(layernorm_kernel<12>, grid, block, 0, st, x, yo, g, b, rows, eps, T, skip_cls); break;
     case 1024: hipLaunchKernelGGL(layernorm_kernel<16>, grid, block, 0, st, x, yo, g, b, rows, eps, T, skip_cls); break;

@@ -1,5 +1,6 @@
 // libmde_hip engine: packed-weight loader, execution context and the DA-V2
-// forward schedule, behind the C ABI of include/mde.h.
+// forward schedule, behind the C ABI of include/mde.h.  The Depth Pro
+// schedule lives in depth_pro.hip; both share engine_internal.h.
 //
 // Replaces TensorRT's ICudaEngine / IExecutionContext as used by the
 // reference (core/common.py:141-312, core/common_runtime.py:131-275): one
@@ -11,15 +12,8 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
-#include <map>
-#include <string>
-#include <tuple>
-#include <unordered_map>
-#include <vector>
 
-#include "../../include/mde.h"
-#include "mde_ops.h"
-#include "pack_format.h"
+#include "engine_internal.h"
 
 using namespace mde;
 
@@ -43,137 +37,15 @@ int hip_fail(hipError_t e, const char* what) {
     if (e_ != hipSuccess) return hip_fail(e_, what); \
   } while (0)
 
-struct DevTensor {
-  void* ptr = nullptr;
-  int dtype = 0;
-  int ndim = 0;
-  int dims[4] = {0, 0, 0, 0};
-};
-
-inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
-
-}  // namespace
-
-struct mde_engine {
-  int device = 0;
-  PackConfig cfg{};
-  void* wmem = nullptr;
-  size_t wbytes = 0;
-  std::unordered_map<std::string, DevTensor> t;
-  // derived geometry
-  int ph = 0, pw = 0, np = 0, T = 0, Tpad = 0, D = 0, H = 0, F = 0;
-  int h4 = 0, w4 = 0;
-  int c1p = 0;          // reassemble-0 channels padded to a multiple of 32 (direct-conv input)
-  float head_b2 = 0.f;  // output_conv2.2 bias (scalar kernel argument)
-
-  const DevTensor* get(const std::string& n) const {
-    auto it = t.find(n);
-    return it == t.end() ? nullptr : &it->second;
-  }
-};
-
-namespace {
-
-struct Buf {
-  h16 *P, *Hn, *Q, *K, *Vt, *O, *Mh;
-  float* X;
-  h16 *tap[4], *pj[4], *l1, *l2, *l4, *rn[4];
-  h16 *tb, *sb, *ub, *vb, *p4, *p3, *p2, *c1;
-  unsigned* lncnt;  // fused-LayerNorm row-block arrival counters (zeroed, self-resetting)
-};
-
-struct GraphKey {
-  int batch;
-  void* in;
-  void* out;
-  bool operator<(const GraphKey& o) const { return std::tie(batch, in, out) < std::tie(o.batch, o.in, o.out); }
-};
-
-}  // namespace
-
-struct mde_context {
-  mde_engine* e = nullptr;
-  int device = 0;
-  int max_batch = 1;
-  int batch = 1;
-  void* in = nullptr;
-  void* out = nullptr;
-  void* arena = nullptr;
-  size_t arena_bytes = 0;
-  Buf b{};
-  bool graph_mode = true;
-  hipStream_t cap_stream = nullptr;
-  std::map<GraphKey, std::pair<hipGraph_t, hipGraphExec_t>> graphs;
-  mde_layer_cb prof_cb = nullptr;
-  void* prof_user = nullptr;
-  std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> prof_events;
-  size_t prof_used = 0;
-};
-
-namespace {
-
-int load_pack(const uint8_t* data, size_t n, int device, mde_engine** out) {
-  if (n < sizeof(PackHeader) + sizeof(PackConfig)) return fail(MDE_ERR_FORMAT, "packed engine truncated");
-  PackHeader hd;
-  memcpy(&hd, data, sizeof hd);
-  if (memcmp(hd.magic, "MDEPACK1", 8) != 0) return fail(MDE_ERR_FORMAT, "bad magic (not an mde packed engine)");
-  if (hd.version != kPackVersion)
-    return fail(MDE_ERR_FORMAT, "packed engine version " + std::to_string(hd.version) + ", expected " +
-                                    std::to_string(kPackVersion));
-  const size_t tab = sizeof(PackHeader) + sizeof(PackConfig);
-  if (tab + (size_t)hd.n_tensors * sizeof(PackTensor) > n || hd.data_offset + hd.data_bytes > n ||
-      hd.data_offset < tab + (size_t)hd.n_tensors * sizeof(PackTensor))
-    return fail(MDE_ERR_FORMAT, "packed engine tables out of range");
-  auto* e = new mde_engine();
-  e->device = device;
-  memcpy(&e->cfg, data + sizeof(PackHeader), sizeof(PackConfig));
+// DA-V2 load-time checks and derived geometry
+std::string setup_dav2(mde_engine* e) {
   const PackConfig& c = e->cfg;
   if (c.patch != 14 || c.embed_dim % 64 || c.num_heads * 64 != c.embed_dim || c.img_h % 14 || c.img_w % 14 ||
-      c.img_h <= 0 || c.img_w <= 0 || c.features % 16 || c.head_hidden != 32) {
-    delete e;
-    return fail(MDE_ERR_FORMAT, "unsupported model geometry in packed config");
-  }
-  if (c.input_u8 != 0 && c.input_u8 != 1) {
-    delete e;
-    return fail(MDE_ERR_FORMAT, "bad input format in packed config");
-  }
-  if (c.input_u8 && (c.in_scale == 0.f || c.in_std[0] == 0.f || c.in_std[1] == 0.f || c.in_std[2] == 0.f)) {
-    delete e;
-    return fail(MDE_ERR_FORMAT, "uint8 input preamble with a zero scale/std");
-  }
-  hipError_t he = hipSetDevice(device);
-  if (he != hipSuccess) {
-    delete e;
-    return hip_fail(he, "hipSetDevice");
-  }
-  e->wbytes = hd.data_bytes;
-  he = hipMalloc(&e->wmem, std::max<size_t>(hd.data_bytes, 256));
-  if (he != hipSuccess) {
-    delete e;
-    return hip_fail(he, "hipMalloc(weights)");
-  }
-  he = hipMemcpy(e->wmem, data + hd.data_offset, hd.data_bytes, hipMemcpyHostToDevice);
-  if (he != hipSuccess) {
-    hipFree(e->wmem);
-    delete e;
-    return hip_fail(he, "hipMemcpy(weights)");
-  }
-  for (uint32_t i = 0; i < hd.n_tensors; ++i) {
-    PackTensor pt;
-    memcpy(&pt, data + tab + (size_t)i * sizeof(PackTensor), sizeof pt);
-    if (pt.offset + pt.nbytes > hd.data_bytes || pt.ndim < 1 || pt.ndim > 4) {
-      hipFree(e->wmem);
-      delete e;
-      return fail(MDE_ERR_FORMAT, "tensor record out of range");
-    }
-    DevTensor dt;
-    dt.ptr = (uint8_t*)e->wmem + pt.offset;
-    dt.dtype = pt.dtype;
-    dt.ndim = pt.ndim;
-    for (int k = 0; k < 4; ++k) dt.dims[k] = pt.dims[k];
-    pt.name[sizeof(pt.name) - 1] = 0;
-    e->t[pt.name] = dt;
-  }
+      c.img_h <= 0 || c.img_w <= 0 || c.features % 16 || c.head_hidden != 32)
+    return "unsupported model geometry in packed config";
+  if (c.input_u8 != 0 && c.input_u8 != 1) return "bad input format in packed config";
+  if (c.input_u8 && (c.in_scale == 0.f || c.in_std[0] == 0.f || c.in_std[1] == 0.f || c.in_std[2] == 0.f))
+    return "uint8 input preamble with a zero scale/std";
   e->D = c.embed_dim;
   e->H = c.num_heads;
   e->F = c.features;
@@ -209,57 +81,121 @@ int load_pack(const uint8_t* data, size_t n, int device, mde_engine** out) {
       }
   }
   for (auto& s : need)
-    if (!e->get(s)) {
-      hipFree(e->wmem);
-      std::string m = "packed engine lacks tensor '" + s + "'";
+    if (!e->get(s)) return "packed engine lacks tensor '" + s + "'";
+  return "";
+}
+
+int load_pack(const uint8_t* data, size_t n, int device, mde_engine** out) {
+  if (n < sizeof(PackHeader) + sizeof(PackConfig)) return fail(MDE_ERR_FORMAT, "packed engine truncated");
+  PackHeader hd;
+  memcpy(&hd, data, sizeof hd);
+  if (memcmp(hd.magic, "MDEPACK1", 8) != 0) return fail(MDE_ERR_FORMAT, "bad magic (not an mde packed engine)");
+  if (hd.version != kPackVersion)
+    return fail(MDE_ERR_FORMAT, "packed engine version " + std::to_string(hd.version) + ", expected " +
+                                    std::to_string(kPackVersion));
+  const size_t tab = sizeof(PackHeader) + sizeof(PackConfig);
+  if (tab + (size_t)hd.n_tensors * sizeof(PackTensor) > n || hd.data_offset + hd.data_bytes > n ||
+      hd.data_offset < tab + (size_t)hd.n_tensors * sizeof(PackTensor))
+    return fail(MDE_ERR_FORMAT, "packed engine tables out of range");
+  auto* e = new mde_engine();
+  e->device = device;
+  memcpy(&e->cfg, data + sizeof(PackHeader), sizeof(PackConfig));
+  e->family = e->cfg.family;
+  if (e->family != FAMILY_DAV2 && e->family != FAMILY_DEPTH_PRO) {
+    delete e;
+    return fail(MDE_ERR_FORMAT, "unknown model family in packed config");
+  }
+  for (uint32_t i = 0; i < hd.n_tensors; ++i) {
+    PackTensor pt;
+    memcpy(&pt, data + tab + (size_t)i * sizeof(PackTensor), sizeof pt);
+    if (pt.offset + pt.nbytes > hd.data_bytes || pt.ndim < 1 || pt.ndim > 4) {
       delete e;
-      return fail(MDE_ERR_FORMAT, m);
+      return fail(MDE_ERR_FORMAT, "tensor record out of range");
     }
+    DevTensor dt;
+    dt.ptr = (void*)(uintptr_t)pt.offset;  // rebased after the upload
+    dt.dtype = pt.dtype;
+    dt.ndim = pt.ndim;
+    for (int k = 0; k < 4; ++k) dt.dims[k] = pt.dims[k];
+    pt.name[sizeof(pt.name) - 1] = 0;
+    e->t[pt.name] = dt;
+  }
+  const std::string bad = e->family == FAMILY_DAV2 ? setup_dav2(e) : setup_depth_pro(e);
+  if (!bad.empty()) {
+    delete e;
+    return fail(MDE_ERR_FORMAT, bad);
+  }
+  hipError_t he = hipSetDevice(device);
+  if (he != hipSuccess) {
+    delete e;
+    return hip_fail(he, "hipSetDevice");
+  }
+  e->wbytes = hd.data_bytes;
+  he = hipMalloc(&e->wmem, std::max<size_t>(hd.data_bytes, 256));
+  if (he != hipSuccess) {
+    delete e;
+    return hip_fail(he, "hipMalloc(weights)");
+  }
+  he = hipMemcpy(e->wmem, data + hd.data_offset, hd.data_bytes, hipMemcpyHostToDevice);
+  if (he != hipSuccess) {
+    hipFree(e->wmem);
+    delete e;
+    return hip_fail(he, "hipMemcpy(weights)");
+  }
+  for (auto& kv : e->t) kv.second.ptr = (uint8_t*)e->wmem + (uintptr_t)kv.second.ptr;
   *out = e;
   return MDE_OK;
 }
 
-// ---- activation arena -----------------------------------------------------
-size_t plan_arena(const mde_engine& e, int B, Buf* b, uint8_t* base) {
-  size_t off = 0;
-  auto take = [&](size_t bytes) -> void* {
-    void* p = base ? (void*)(base + off) : nullptr;
-    off += align_up(bytes, 256);
-    return p;
-  };
+}  // namespace
+
+namespace mde {
+
+// ---- DA-V2 activation arena ---------------------------------------------------
+size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
+  ArenaPlan a(base);
   const size_t bb = (size_t)B;
   const int D = e.D, F = e.F, np = e.np;
   const int* oc = e.cfg.out_channels;
   const size_t s1 = (size_t)(4 * e.ph) * (4 * e.pw), s2 = (size_t)(2 * e.ph) * (2 * e.pw), s3 = np,
                s4 = (size_t)e.h4 * e.w4;
   const size_t s0 = (size_t)(8 * e.ph) * (8 * e.pw);
-  Buf t{};
-  t.P = (h16*)take(bb * np * 672 * 2);
-  t.X = (float*)take(bb * e.T * D * 4);
-  t.Hn = (h16*)take(bb * e.T * D * 2);
-  t.Q = (h16*)take(bb * e.H * e.Tpad * 64 * 2);
-  t.K = (h16*)take(bb * e.H * e.Tpad * 64 * 2);
-  t.Vt = (h16*)take(bb * e.H * e.Tpad * 64 * 2);
-  t.O = (h16*)take(bb * e.T * D * 2);
-  t.Mh = (h16*)take(bb * e.T * e.cfg.mlp_hidden * 2);
-  for (int i = 0; i < 4; ++i) t.tap[i] = (h16*)take(bb * np * D * 2);
-  for (int i = 0; i < 4; ++i) t.pj[i] = (h16*)take(bb * np * oc[i] * 2);
-  t.l1 = (h16*)take(bb * s1 * e.c1p * 2);  // channels padded to a multiple of 32 (pad stays 0)
-  t.l2 = (h16*)take(bb * s2 * oc[1] * 2);
-  t.l4 = (h16*)take(bb * s4 * oc[3] * 2);
+  DAV2Buf t{};
+  t.P = a.h(bb * np * 672);
+  t.X = a.f(bb * e.T * D);
+  t.Hn = a.h(bb * e.T * D);
+  t.Q = a.h(bb * e.H * e.Tpad * 64);
+  t.K = a.h(bb * e.H * e.Tpad * 64);
+  t.Vt = a.h(bb * e.H * e.Tpad * 64);
+  t.O = a.h(bb * e.T * D);
+  t.Mh = a.h(bb * e.T * e.cfg.mlp_hidden);
+  for (int i = 0; i < 4; ++i) t.tap[i] = a.h(bb * np * D);
+  for (int i = 0; i < 4; ++i) t.pj[i] = a.h(bb * np * oc[i]);
+  t.l1 = a.h(bb * s1 * e.c1p);  // channels padded to a multiple of 32 (pad stays 0)
+  t.l2 = a.h(bb * s2 * oc[1]);
+  t.l4 = a.h(bb * s4 * oc[3]);
   const size_t ss[4] = {s1, s2, s3, s4};
-  for (int i = 0; i < 4; ++i) t.rn[i] = (h16*)take(bb * ss[i] * F * 2);
-  t.tb = (h16*)take(bb * s1 * F * 2);
-  t.sb = (h16*)take(bb * s1 * F * 2);
-  t.ub = (h16*)take(bb * s1 * F * 2);
-  t.vb = (h16*)take(bb * s1 * F * 2);
-  t.p4 = (h16*)take(bb * s3 * F * 2);
-  t.p3 = (h16*)take(bb * s2 * F * 2);
-  t.p2 = (h16*)take(bb * s1 * F * 2);
-  t.c1 = (h16*)take(bb * s0 * (F / 2) * 2);
-  t.lncnt = (unsigned*)take((bb * e.T / 32 + 1) * 4);  // >= one word per 32-row block
+  for (int i = 0; i < 4; ++i) t.rn[i] = a.h(bb * ss[i] * F);
+  t.tb = a.h(bb * s1 * F);
+  t.sb = a.h(bb * s1 * F);
+  t.ub = a.h(bb * s1 * F);
+  t.vb = a.h(bb * s1 * F);
+  t.p4 = a.h(bb * s3 * F);
+  t.p3 = a.h(bb * s2 * F);
+  t.p2 = a.h(bb * s1 * F);
+  t.c1 = a.h(bb * s0 * (F / 2));
+  t.lncnt = (unsigned*)a.take((bb * e.T / 32 + 1) * 4);  // >= one word per 32-row block
   if (b) *b = t;
-  return off;
+  return a.off;
+}
+
+}  // namespace mde
+
+namespace {
+
+size_t plan_arena(const mde_engine& e, int B, mde_context* c, uint8_t* base) {
+  if (e.family == FAMILY_DEPTH_PRO) return plan_arena_dp(e, B, c ? &c->d : nullptr, base);
+  return plan_arena_dav2(e, B, c ? &c->b : nullptr, base);
 }
 
 // MDE_FUSE_LN=1 folds the LayerNorms into the proj/fc2 epilogues (row-block
@@ -267,7 +203,7 @@ size_t plan_arena(const mde_engine& e, int B, Buf* b, uint8_t* base) {
 // on MI355X (r01: proj 54 -> 113 us, fc2 98 -> 156 us at B=32) because every
 // agent-scope release/acquire writes back / invalidates the XCD's whole L2,
 // evicting the operand tiles of the other workgroups on that XCD.
-static bool fuse_ln_enabled() {
+bool fuse_ln_enabled() {
   static const int v = [] {
     const char* e = getenv("MDE_FUSE_LN");
     return (e && e[0] == '1') ? 1 : 0;
@@ -275,356 +211,273 @@ static bool fuse_ln_enabled() {
   return v != 0;
 }
 
-// ---- the forward schedule ----------------------------------------------------
-struct Runner {
-  mde_context& c;
-  hipStream_t st;
-  bool prof;
-  hipError_t err = hipSuccess;
+}  // namespace
 
-  template <class Fn>
-  void step(const char* name, Fn&& fn) {
-    if (err != hipSuccess) return;
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (prof) {
-      if (c.prof_used >= c.prof_events.size()) {
-        hipEvent_t a, b;
-        if ((err = hipEventCreate(&a)) != hipSuccess) return;
-        if ((err = hipEventCreate(&b)) != hipSuccess) return;
-        c.prof_events.push_back({std::string(), {a, b}});
-      }
-      auto& slot = c.prof_events[c.prof_used++];
-      slot.first = name;
-      e0 = slot.second.first;
-      e1 = slot.second.second;
-      if ((err = hipEventRecord(e0, st)) != hipSuccess) return;
+namespace mde {
+
+// FeatureFusionBlock: [x0 + RCU1(x1)] -> RCU2 -> out_conv(1x1) -> resize.
+// The 1x1 out_conv is applied BEFORE the bilinear resize (both are linear
+// and bilinear weights sum to 1, so they commute exactly in real
+// arithmetic); this runs the 1x1 GEMM on 4x fewer pixels.
+void Runner::dav2_fusion(int r, const h16* x0, const h16* x1, int B, int h, int w, h16* dst, int oh, int ow) {
+  const std::string p = "rf" + std::to_string(r);
+  const int F = c.e->F;
+  const h16* s = x0;
+  if (x1) {
+    rcu(p + ".rcu1", x1, x0, c.b.sb, c.b.tb, B, h, w, F);
+    s = c.b.sb;
+  }
+  rcu(p + ".rcu2", s, nullptr, c.b.ub, c.b.tb, B, h, w, F);
+  GemmParams g = dense(c.b.ub, F, p + ".out.w", B * h * w, F, F);
+  g.emode = E_STORE;
+  g.bias = w32(p + ".out.b");
+  g.out16 = c.b.vb;
+  g.ldo = F;
+  gemm((p + ".out").c_str(), g);
+  if (dst) step((p + ".resize").c_str(), [&] { return launch_resize(c.b.vb, dst, B, h, w, F, oh, ow, st); });
+}
+
+hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
+  mde_engine& e = *c.e;
+  const PackConfig& cf = e.cfg;
+  const int D = e.D, T = e.T, np = e.np, F = e.F;
+  const int* oc = cf.out_channels;
+  DAV2Buf& b = c.b;
+
+  step("patch_prep", [&] {
+    if (cf.input_u8)
+      return launch_patch_prep_u8((const unsigned char*)img, b.P, b.X, w32("pos.cls"), B, cf.img_h, cf.img_w, e.ph,
+                                  e.pw, T, D, cf.in_scale, cf.in_mean, cf.in_std, st);
+    return launch_patch_prep((const float*)img, b.P, b.X, w32("pos.cls"), B, cf.img_h, cf.img_w, e.ph, e.pw, T, D,
+                             st);
+  });
+  {
+    GemmParams g = dense(b.P, 672, "patch.w", B * np, D, 672);
+    g.emode = E_PATCH;
+    g.bias = w32("patch.b");
+    g.x32 = b.X;
+    g.ldo = D;
+    g.T = T;
+    g.pos = w32("pos.patch");
+    g.npatch = np;
+    gemm("patch_embed", g);
+  }
+  int tap = 0;
+  char nm[64];
+  const bool fuse = fuse_ln_enabled() && (D == 384 || D == 768 || D == 1024);
+  // fused LayerNorm in a residual GEMM's tail: out1 = LN(g1,b1) (token
+  // layout), out2 = final norm into a tap map (cls dropped)
+  auto fuse_ln = [&](GemmParams& g, const char* g1, const char* b1, h16* tapdst) {
+    if (!fuse) return;
+    g.ln_counter = b.lncnt;
+    g.ln_eps = cf.ln_eps;
+    g.ln_T = T;
+    if (g1) {
+      g.ln1_g = w32(g1);
+      g.ln1_b = w32(b1);
+      g.ln1_out = b.Hn;
     }
-    err = fn();
-    if (err == hipSuccess && prof) err = hipEventRecord(e1, st);
-  }
-
-  const DevTensor& W(const std::string& n) { return *c.e->get(n); }
-  const h16* w16(const std::string& n) { return (const h16*)W(n).ptr; }
-  const float* w32(const std::string& n) { return (const float*)W(n).ptr; }
-  int ldw(const std::string& n) { return W(n).dims[W(n).ndim - 1]; }
-
-  GemmParams dense(const h16* A, int lda, const std::string& w, int M, int N, int K) {
-    GemmParams g;
-    g.amode = A_DENSE;
-    g.A = A;
-    g.lda = lda;
-    g.W = w16(w);
-    g.ldw = ldw(w);
-    g.M = M;
-    g.N = N;
-    g.K = K;
-    return g;
-  }
-
-  // 3x3 pad-1 conv over NHWC map [B][h][w][cin] -> [B][ho][wo][cout]
-  GemmParams conv(const h16* in, int B, int h, int w, int cin, const std::string& wn, int cout, int stride) {
-    GemmParams g;
-    g.amode = A_CONV3;
-    g.A = in;
-    g.cb = B;
-    g.ch = h;
-    g.cw = w;
-    g.cc = cin;
-    g.stride = stride;
-    g.oh = (h - 1) / stride + 1;
-    g.ow = (w - 1) / stride + 1;
-    g.W = w16(wn);
-    g.ldw = ldw(wn);
-    g.M = B * g.oh * g.ow;
-    g.N = cout;
-    g.K = 9 * cin;
-    g.out16 = nullptr;
-    g.ldo = cout;
-    return g;
-  }
-
-  void gemm(const char* name, const GemmParams& g) {
-    step(name, [&] { return launch_gemm(g, st); });
-  }
-
-  // RCU (pre-activation residual conv unit) at one scale:
-  // out = conv2(relu(conv1(relu(x)) + b1)) + b2 + x (+ extra)
-  void rcu(const std::string& pfx, const h16* x, const h16* extra, h16* out, int B, int h, int w) {
-    const int F = c.e->F;
-    GemmParams g1 = conv(x, B, h, w, F, pfx + ".c1.w", F, 1);
-    g1.relu_in = 1;
-    g1.bias = w32(pfx + ".c1.b");
-    g1.act = ACT_RELU;
-    g1.out16 = c.b.tb;
-    gemm((pfx + ".c1").c_str(), g1);
-    GemmParams g2 = conv(c.b.tb, B, h, w, F, pfx + ".c2.w", F, 1);
-    g2.bias = w32(pfx + ".c2.b");
-    g2.res0 = x;
-    g2.res1 = extra;
-    g2.out16 = out;
-    gemm((pfx + ".c2").c_str(), g2);
-  }
-
-  // FeatureFusionBlock: [x0 + RCU1(x1)] -> RCU2 -> out_conv(1x1) -> resize.
-  // The 1x1 out_conv is applied BEFORE the bilinear resize (both are linear
-  // and bilinear weights sum to 1, so they commute exactly in real
-  // arithmetic); this runs the 1x1 GEMM on 4x fewer pixels.
-  void fusion(int r, const h16* x0, const h16* x1, int B, int h, int w, h16* dst, int oh, int ow) {
-    const std::string p = "rf" + std::to_string(r);
-    const int F = c.e->F;
-    const h16* s = x0;
-    if (x1) {
-      rcu(p + ".rcu1", x1, x0, c.b.sb, B, h, w);
-      s = c.b.sb;
+    if (tapdst) {
+      g.ln2_g = w32("norm.g");
+      g.ln2_b = w32("norm.b");
+      g.ln2_out = tapdst;
+      g.ln2_skip = 1;
     }
-    rcu(p + ".rcu2", s, nullptr, c.b.ub, B, h, w);
-    GemmParams g = dense(c.b.ub, F, p + ".out.w", B * h * w, F, F);
-    g.emode = E_STORE;
-    g.bias = w32(p + ".out.b");
-    g.out16 = c.b.vb;
-    g.ldo = F;
-    gemm((p + ".out").c_str(), g);
-    if (dst) step((p + ".resize").c_str(), [&] { return launch_resize(c.b.vb, dst, B, h, w, F, oh, ow, st); });
-  }
-
-  hipError_t forward(int B, const void* img, float* out) {
-    mde_engine& e = *c.e;
-    const PackConfig& cf = e.cfg;
-    const int D = e.D, T = e.T, np = e.np, F = e.F;
-    const int* oc = cf.out_channels;
-    Buf& b = c.b;
-
-    step("patch_prep", [&] {
-      if (cf.input_u8)
-        return launch_patch_prep_u8((const unsigned char*)img, b.P, b.X, w32("pos.cls"), B, cf.img_h, cf.img_w, e.ph,
-                                    e.pw, T, D, cf.in_scale, cf.in_mean, cf.in_std, st);
-      return launch_patch_prep((const float*)img, b.P, b.X, w32("pos.cls"), B, cf.img_h, cf.img_w, e.ph, e.pw, T, D,
-                               st);
-    });
+  };
+  for (int i = 0; i < cf.depth; ++i) {
+    const std::string p = "b" + std::to_string(i) + ".";
+    const std::string pn = "b" + std::to_string(i + 1) + ".";
+    if (!fuse || i == 0) {
+      snprintf(nm, sizeof nm, "block%d.norm1", i);
+      step(nm, [&] {
+        return launch_layernorm(b.X, b.Hn, w32(p + "ln1.g"), w32(p + "ln1.b"), B * T, D, cf.ln_eps, T, 0, st);
+      });
+    }
     {
-      GemmParams g = dense(b.P, 672, "patch.w", B * np, D, 672);
-      g.emode = E_PATCH;
-      g.bias = w32("patch.b");
+      GemmParams g = dense(b.Hn, D, p + "qkv.w", B * T, 3 * D, D);
+      g.emode = E_QKV;
+      g.bias = w32(p + "qkv.b");
+      g.q = b.Q;
+      g.k = b.K;
+      g.vt = b.Vt;
+      g.T = T;
+      g.Tpad = e.Tpad;
+      g.heads = e.H;
+      g.qscale = 0.125f * 1.4426950408889634f;  // dh^-0.5 * log2(e): scores in log2 units
+      snprintf(nm, sizeof nm, "block%d.qkv", i);
+      gemm(nm, g);
+    }
+    snprintf(nm, sizeof nm, "block%d.attn", i);
+    step(nm, [&] { return launch_attention(b.Q, b.K, b.Vt, b.O, B, e.H, T, e.Tpad, D, st); });
+    {
+      GemmParams g = dense(b.O, D, p + "proj.w", B * T, D, D);
+      g.emode = E_RESID;
+      g.bias = w32(p + "proj.b");
+      g.ls = w32(p + "ls1");
       g.x32 = b.X;
       g.ldo = D;
-      g.T = T;
-      g.pos = w32("pos.patch");
-      g.npatch = np;
-      gemm("patch_embed", g);
+      const std::string lg = p + "ln2.g", lb = p + "ln2.b";
+      fuse_ln(g, lg.c_str(), lb.c_str(), nullptr);
+      snprintf(nm, sizeof nm, "block%d.proj", i);
+      gemm(nm, g);
     }
-    int tap = 0;
-    char nm[64];
-    const bool fuse = fuse_ln_enabled() && (D == 384 || D == 768 || D == 1024);
-    // fused LayerNorm in a residual GEMM's tail: out1 = LN(g1,b1) (token
-    // layout), out2 = final norm into a tap map (cls dropped)
-    auto fuse_ln = [&](GemmParams& g, const char* g1, const char* b1, h16* tapdst) {
-      if (!fuse) return;
-      g.ln_counter = b.lncnt;
-      g.ln_eps = cf.ln_eps;
-      g.ln_T = T;
-      if (g1) {
-        g.ln1_g = w32(g1);
-        g.ln1_b = w32(b1);
-        g.ln1_out = b.Hn;
-      }
-      if (tapdst) {
-        g.ln2_g = w32("norm.g");
-        g.ln2_b = w32("norm.b");
-        g.ln2_out = tapdst;
-        g.ln2_skip = 1;
-      }
-    };
-    for (int i = 0; i < cf.depth; ++i) {
-      const std::string p = "b" + std::to_string(i) + ".";
-      const std::string pn = "b" + std::to_string(i + 1) + ".";
-      if (!fuse || i == 0) {
-        snprintf(nm, sizeof nm, "block%d.norm1", i);
-        step(nm, [&] {
-          return launch_layernorm(b.X, b.Hn, w32(p + "ln1.g"), w32(p + "ln1.b"), B * T, D, cf.ln_eps, T, 0, st);
-        });
-      }
-      {
-        GemmParams g = dense(b.Hn, D, p + "qkv.w", B * T, 3 * D, D);
-        g.emode = E_QKV;
-        g.bias = w32(p + "qkv.b");
-        g.q = b.Q;
-        g.k = b.K;
-        g.vt = b.Vt;
-        g.T = T;
-        g.Tpad = e.Tpad;
-        g.heads = e.H;
-        g.qscale = 0.125f * 1.4426950408889634f;  // dh^-0.5 * log2(e): scores in log2 units
-        snprintf(nm, sizeof nm, "block%d.qkv", i);
-        gemm(nm, g);
-      }
-      snprintf(nm, sizeof nm, "block%d.attn", i);
-      step(nm, [&] { return launch_attention(b.Q, b.K, b.Vt, b.O, B, e.H, T, e.Tpad, D, st); });
-      {
-        GemmParams g = dense(b.O, D, p + "proj.w", B * T, D, D);
-        g.emode = E_RESID;
-        g.bias = w32(p + "proj.b");
-        g.ls = w32(p + "ls1");
-        g.x32 = b.X;
-        g.ldo = D;
-        const std::string lg = p + "ln2.g", lb = p + "ln2.b";
-        fuse_ln(g, lg.c_str(), lb.c_str(), nullptr);
-        snprintf(nm, sizeof nm, "block%d.proj", i);
-        gemm(nm, g);
-      }
-      if (!fuse) {
-        snprintf(nm, sizeof nm, "block%d.norm2", i);
-        step(nm, [&] {
-          return launch_layernorm(b.X, b.Hn, w32(p + "ln2.g"), w32(p + "ln2.b"), B * T, D, cf.ln_eps, T, 0, st);
-        });
-      }
-      {
-        GemmParams g = dense(b.Hn, D, p + "fc1.w", B * T, cf.mlp_hidden, D);
-        g.emode = E_STORE;
-        g.bias = w32(p + "fc1.b");
-        g.act = ACT_GELU;
-        g.out16 = b.Mh;
-        g.ldo = cf.mlp_hidden;
-        snprintf(nm, sizeof nm, "block%d.fc1", i);
-        gemm(nm, g);
-      }
-      {
-        GemmParams g = dense(b.Mh, cf.mlp_hidden, p + "fc2.w", B * T, D, cf.mlp_hidden);
-        g.emode = E_RESID;
-        g.bias = w32(p + "fc2.b");
-        g.ls = w32(p + "ls2");
-        g.x32 = b.X;
-        g.ldo = D;
-        const bool tapped = tap < 4 && cf.taps[tap] == i;
-        const std::string lg = pn + "ln1.g", lb = pn + "ln1.b";
-        fuse_ln(g, i + 1 < cf.depth ? lg.c_str() : nullptr, lb.c_str(), tapped ? b.tap[tap] : nullptr);
-        snprintf(nm, sizeof nm, "block%d.fc2", i);
-        gemm(nm, g);
-      }
-      if (fuse && tap < 4 && cf.taps[tap] == i) {
-        ++tap;
-      } else if (tap < 4 && cf.taps[tap] == i) {
-        snprintf(nm, sizeof nm, "tap%d.norm", tap);
-        h16* dst = b.tap[tap];
-        step(nm, [&] {
-          return launch_layernorm(b.X, dst, w32("norm.g"), w32("norm.b"), B * T, D, cf.ln_eps, T, 1, st);
-        });
-        ++tap;
-      }
+    if (!fuse) {
+      snprintf(nm, sizeof nm, "block%d.norm2", i);
+      step(nm, [&] {
+        return launch_layernorm(b.X, b.Hn, w32(p + "ln2.g"), w32(p + "ln2.b"), B * T, D, cf.ln_eps, T, 0, st);
+      });
     }
-    if (tap != 4) return hipErrorInvalidValue;
-
-    // ---- DPT head: reassemble ----
-    for (int i = 0; i < 4; ++i) {
-      GemmParams g = dense(b.tap[i], D, "proj" + std::to_string(i) + ".w", B * np, oc[i], D);
+    {
+      GemmParams g = dense(b.Hn, D, p + "fc1.w", B * T, cf.mlp_hidden, D);
       g.emode = E_STORE;
-      g.bias = w32("proj" + std::to_string(i) + ".b");
-      g.out16 = b.pj[i];
-      g.ldo = oc[i];
-      snprintf(nm, sizeof nm, "reassemble%d.project", i);
+      g.bias = w32(p + "fc1.b");
+      g.act = ACT_GELU;
+      g.out16 = b.Mh;
+      g.ldo = cf.mlp_hidden;
+      snprintf(nm, sizeof nm, "block%d.fc1", i);
       gemm(nm, g);
     }
     {
-      GemmParams g = dense(b.pj[0], oc[0], "rs0.w", B * np, 16 * oc[0], oc[0]);
-      g.emode = E_CONVT;
-      g.bias = w32("rs0.b");
-      g.out16 = b.l1;
-      g.s = 4;
-      g.cout = oc[0];
-      g.ldo = e.c1p;
-      g.ih = e.ph;
-      g.iw = e.pw;
-      gemm("reassemble0.convT4", g);
-    }
-    {
-      GemmParams g = dense(b.pj[1], oc[1], "rs1.w", B * np, 4 * oc[1], oc[1]);
-      g.emode = E_CONVT;
-      g.bias = w32("rs1.b");
-      g.out16 = b.l2;
-      g.s = 2;
-      g.cout = oc[1];
-      g.ldo = oc[1];
-      g.ih = e.ph;
-      g.iw = e.pw;
-      gemm("reassemble1.convT2", g);
-    }
-    {
-      GemmParams g = conv(b.pj[3], B, e.ph, e.pw, oc[3], "rs3.w", oc[3], 2);
-      g.bias = w32("rs3.b");
-      g.out16 = b.l4;
-      gemm("reassemble3.conv_s2", g);
-    }
-    const int hs[4] = {4 * e.ph, 2 * e.ph, e.ph, e.h4};
-    const int ws[4] = {4 * e.pw, 2 * e.pw, e.pw, e.w4};
-    const h16* lay[4] = {b.l1, b.l2, b.pj[2], b.l4};
-    const int cin[4] = {e.c1p, oc[1], oc[2], oc[3]};
-    for (int i = 0; i < 4; ++i) {
-      GemmParams g = conv(lay[i], B, hs[i], ws[i], cin[i], "rn" + std::to_string(i + 1) + ".w", F, 1);
-      g.out16 = b.rn[i];
-      snprintf(nm, sizeof nm, "layer%d_rn", i + 1);
+      GemmParams g = dense(b.Mh, cf.mlp_hidden, p + "fc2.w", B * T, D, cf.mlp_hidden);
+      g.emode = E_RESID;
+      g.bias = w32(p + "fc2.b");
+      g.ls = w32(p + "ls2");
+      g.x32 = b.X;
+      g.ldo = D;
+      const bool tapped = tap < 4 && cf.taps[tap] == i;
+      const std::string lg = pn + "ln1.g", lb = pn + "ln1.b";
+      fuse_ln(g, i + 1 < cf.depth ? lg.c_str() : nullptr, lb.c_str(), tapped ? b.tap[tap] : nullptr);
+      snprintf(nm, sizeof nm, "block%d.fc2", i);
       gemm(nm, g);
     }
-    // ---- fusion (refinenet4 .. refinenet1) ----
-    fusion(4, b.rn[3], nullptr, B, hs[3], ws[3], b.p4, hs[2], ws[2]);
-    fusion(3, b.p4, b.rn[2], B, hs[2], ws[2], b.p3, hs[1], ws[1]);
-    fusion(2, b.p3, b.rn[1], B, hs[1], ws[1], b.p2, hs[0], ws[0]);
-    fusion(1, b.p2, b.rn[0], B, hs[0], ws[0], nullptr, 0, 0);  // 1x1 result in vb at hs[0] x ws[0]
-    // ---- head ----
-    const int H1 = 2 * hs[0], W1 = 2 * ws[0];  // refinenet1 upsample x2 (fused into output_conv1's loader)
-    {
-      GemmParams g;
-      g.amode = A_CONV3_UP;
-      g.emode = E_STORE;
-      g.A = b.vb;
-      g.cb = B;
-      g.ch = hs[0];
-      g.cw = ws[0];
-      g.cc = F;
-      g.uh = H1;
-      g.uw = W1;
-      g.oh = H1;
-      g.ow = W1;
-      g.stride = 1;
-      g.W = w16("head.c1.w");
-      g.ldw = ldw("head.c1.w");
-      g.M = B * H1 * W1;
-      g.N = F / 2;
-      g.K = 9 * F;
-      g.bias = w32("head.c1.b");
-      g.out16 = b.c1;
-      g.ldo = F / 2;
-      gemm("head.output_conv1", g);
+    if (fuse && tap < 4 && cf.taps[tap] == i) {
+      ++tap;
+    } else if (tap < 4 && cf.taps[tap] == i) {
+      snprintf(nm, sizeof nm, "tap%d.norm", tap);
+      h16* dst = b.tap[tap];
+      step(nm, [&] {
+        return launch_layernorm(b.X, dst, w32("norm.g"), w32("norm.b"), B * T, D, cf.ln_eps, T, 1, st);
+      });
+      ++tap;
     }
-    {
-      const int OH = cf.img_h, OW = cf.img_w;  // (ph*14, pw*14)
-      GemmParams g;
-      g.amode = A_CONV3_UP;
-      g.emode = E_HEAD;
-      g.A = b.c1;
-      g.cb = B;
-      g.ch = H1;
-      g.cw = W1;
-      g.cc = F / 2;
-      g.uh = OH;
-      g.uw = OW;
-      g.oh = OH;
-      g.ow = OW;
-      g.stride = 1;
-      g.W = w16("head.c2.w");
-      g.ldw = ldw("head.c2.w");
-      g.M = B * OH * OW;
-      g.N = cf.head_hidden;
-      g.K = 9 * (F / 2);
-      g.bias = w32("head.c2.b");
-      g.w2 = w32("head.c3.w");
-      g.b2 = e.head_b2;
-      g.head_metric = cf.metric;
-      g.max_depth = cf.max_depth;
-      g.out32 = out;
-      gemm("head.output_conv2", g);
-    }
-    return err;
   }
-};
+  if (tap != 4) return hipErrorInvalidValue;
+
+  // ---- DPT head: reassemble ----
+  for (int i = 0; i < 4; ++i) {
+    GemmParams g = dense(b.tap[i], D, "proj" + std::to_string(i) + ".w", B * np, oc[i], D);
+    g.emode = E_STORE;
+    g.bias = w32("proj" + std::to_string(i) + ".b");
+    g.out16 = b.pj[i];
+    g.ldo = oc[i];
+    snprintf(nm, sizeof nm, "reassemble%d.project", i);
+    gemm(nm, g);
+  }
+  {
+    GemmParams g = dense(b.pj[0], oc[0], "rs0.w", B * np, 16 * oc[0], oc[0]);
+    g.emode = E_CONVT;
+    g.bias = w32("rs0.b");
+    g.out16 = b.l1;
+    g.s = 4;
+    g.cout = oc[0];
+    g.ldo = e.c1p;
+    g.ih = e.ph;
+    g.iw = e.pw;
+    gemm("reassemble0.convT4", g);
+  }
+  {
+    GemmParams g = dense(b.pj[1], oc[1], "rs1.w", B * np, 4 * oc[1], oc[1]);
+    g.emode = E_CONVT;
+    g.bias = w32("rs1.b");
+    g.out16 = b.l2;
+    g.s = 2;
+    g.cout = oc[1];
+    g.ldo = oc[1];
+    g.ih = e.ph;
+    g.iw = e.pw;
+    gemm("reassemble1.convT2", g);
+  }
+  {
+    GemmParams g = conv(b.pj[3], B, e.ph, e.pw, oc[3], "rs3.w", oc[3], 2);
+    g.bias = w32("rs3.b");
+    g.out16 = b.l4;
+    gemm("reassemble3.conv_s2", g);
+  }
+  const int hs[4] = {4 * e.ph, 2 * e.ph, e.ph, e.h4};
+  const int ws[4] = {4 * e.pw, 2 * e.pw, e.pw, e.w4};
+  const h16* lay[4] = {b.l1, b.l2, b.pj[2], b.l4};
+  const int cin[4] = {e.c1p, oc[1], oc[2], oc[3]};
+  for (int i = 0; i < 4; ++i) {
+    GemmParams g = conv(lay[i], B, hs[i], ws[i], cin[i], "rn" + std::to_string(i + 1) + ".w", F, 1);
+    g.out16 = b.rn[i];
+    snprintf(nm, sizeof nm, "layer%d_rn", i + 1);
+    gemm(nm, g);
+  }
+  // ---- fusion (refinenet4 .. refinenet1) ----
+  dav2_fusion(4, b.rn[3], nullptr, B, hs[3], ws[3], b.p4, hs[2], ws[2]);
+  dav2_fusion(3, b.p4, b.rn[2], B, hs[2], ws[2], b.p3, hs[1], ws[1]);
+  dav2_fusion(2, b.p3, b.rn[1], B, hs[1], ws[1], b.p2, hs[0], ws[0]);
+  dav2_fusion(1, b.p2, b.rn[0], B, hs[0], ws[0], nullptr, 0, 0);  // 1x1 result in vb at hs[0] x ws[0]
+  // ---- head ----
+  const int H1 = 2 * hs[0], W1 = 2 * ws[0];  // refinenet1 upsample x2 (fused into output_conv1's loader)
+  {
+    GemmParams g;
+    g.amode = A_CONV3_UP;
+    g.emode = E_STORE;
+    g.A = b.vb;
+    g.cb = B;
+    g.ch = hs[0];
+    g.cw = ws[0];
+    g.cc = F;
+    g.uh = H1;
+    g.uw = W1;
+    g.oh = H1;
+    g.ow = W1;
+    g.stride = 1;
+    g.W = w16("head.c1.w");
+    g.ldw = ldw("head.c1.w");
+    g.M = B * H1 * W1;
+    g.N = F / 2;
+    g.K = 9 * F;
+    g.bias = w32("head.c1.b");
+    g.out16 = b.c1;
+    g.ldo = F / 2;
+    gemm("head.output_conv1", g);
+  }
+  {
+    const int OH = cf.img_h, OW = cf.img_w;  // (ph*14, pw*14)
+    GemmParams g;
+    g.amode = A_CONV3_UP;
+    g.emode = E_HEAD;
+    g.A = b.c1;
+    g.cb = B;
+    g.ch = H1;
+    g.cw = W1;
+    g.cc = F / 2;
+    g.uh = OH;
+    g.uw = OW;
+    g.oh = OH;
+    g.ow = OW;
+    g.stride = 1;
+    g.W = w16("head.c2.w");
+    g.ldw = ldw("head.c2.w");
+    g.M = B * OH * OW;
+    g.N = cf.head_hidden;
+    g.K = 9 * (F / 2);
+    g.bias = w32("head.c2.b");
+    g.w2 = w32("head.c3.w");
+    g.b2 = e.head_b2;
+    g.head_metric = cf.metric;
+    g.max_depth = cf.max_depth;
+    g.out32 = out;
+    gemm("head.output_conv2", g);
+  }
+  return err;
+}
+
+}  // namespace mde
+
+namespace {
 
 int check_ctx(const mde_context* c) {
   if (!c || !c->e) return fail(MDE_ERR_ARG, "null context");
@@ -633,7 +486,23 @@ int check_ctx(const mde_context* c) {
 
 const char* input_name(const mde_engine* e) { return e->cfg.input_u8 ? "image_u8" : "input"; }
 bool is_input(const mde_engine* e, const char* n) { return n && strcmp(n, input_name(e)) == 0; }
-bool is_output(const char* n) { return n && strcmp(n, "output") == 0; }
+
+// io binding index of a tensor name (0 = input, 1 = depth output, 2 = fov), -1 if unknown
+int io_index(const mde_engine* e, const char* n) {
+  if (!n) return -1;
+  int nio = 0;
+  mde_engine_num_io(e, &nio);
+  for (int i = 0; i < nio; ++i) {
+    mde_io_desc d;
+    if (mde_engine_io_desc(e, i, &d) == MDE_OK && strcmp(d.name, n) == 0) return i;
+  }
+  return -1;
+}
+
+hipError_t run_forward(Runner& r, int B, const void* in, float* out, float* out2) {
+  if (r.c.e->family == FAMILY_DEPTH_PRO) return r.forward_dp(B, (const float*)in, out, out2);
+  return r.forward_dav2(B, in, out);
+}
 
 }  // namespace
 
@@ -651,6 +520,8 @@ int mde_engine_load_memory(const void* data, size_t nbytes, int device, mde_engi
   // the head's 1x1 bias scalar, stashed host-side for the kernel argument
   mde_engine* e = *out;
   hipError_t he = hipMemcpy(&e->head_b2, e->get("head.c3.b")->ptr, 4, hipMemcpyDeviceToHost);
+  if (he == hipSuccess && e->family == FAMILY_DEPTH_PRO && e->cfg.use_fov)
+    he = hipMemcpy(&e->fov_b, e->get("fov.final.b")->ptr, 4, hipMemcpyDeviceToHost);
   if (he != hipSuccess) {
     mde_engine_destroy(e);
     *out = nullptr;
@@ -711,12 +582,13 @@ int mde_engine_get_info(const mde_engine* e, mde_engine_info* o) {
   o->max_batch_hint = 64;
   o->weight_bytes = (int64_t)e->wbytes;
   o->input_format = c.input_u8 ? 1 : 0;
+  o->family = e->family;
   return MDE_OK;
 }
 
 int mde_engine_num_io(const mde_engine* e, int* n) {
   if (!e || !n) return fail(MDE_ERR_ARG, "null argument");
-  *n = 2;
+  *n = (e->family == FAMILY_DEPTH_PRO && e->cfg.use_fov) ? 3 : 2;
   return MDE_OK;
 }
 
@@ -741,6 +613,23 @@ int mde_engine_io_desc(const mde_engine* e, int index, mde_io_desc* o) {
     o->dims[1] = 3;
     o->dims[2] = e->cfg.img_h;
     o->dims[3] = e->cfg.img_w;
+  } else if (index == 1 && e->family == FAMILY_DEPTH_PRO) {
+    // reference output_names=["canonical_inverse_depth", "fov_deg"] (models/depth_pro/onnx_export.py:56),
+    // output shape (1, 1, 1536, 1536) (onnx2trt.py:92)
+    strcpy(o->name, "canonical_inverse_depth");
+    o->dtype = MDE_FLOAT32;
+    o->is_input = 0;
+    o->rank = 4;
+    o->dims[0] = -1;
+    o->dims[1] = 1;
+    o->dims[2] = e->cfg.img_h;
+    o->dims[3] = e->cfg.img_w;
+  } else if (index == 2 && e->family == FAMILY_DEPTH_PRO && e->cfg.use_fov) {
+    strcpy(o->name, "fov_deg");
+    o->dtype = MDE_FLOAT32;
+    o->is_input = 0;
+    o->rank = 1;
+    o->dims[0] = -1;
   } else if (index == 1) {
     strcpy(o->name, "output");
     o->dtype = MDE_FLOAT32;
@@ -760,7 +649,7 @@ int mde_engine_profile_shape(const mde_engine* e, const char* name, int which, i
   if (which < 0 || which > 2) return fail(MDE_ERR_ARG, "which must be 0 (min), 1 (opt) or 2 (max)");
   const int64_t bsel[3] = {1, 1, 64};
   mde_io_desc d;
-  int idx = is_input(e, name) ? 0 : is_output(name) ? 1 : -1;
+  int idx = io_index(e, name);
   if (idx < 0) return fail(MDE_ERR_NAME, std::string("unknown tensor ") + name);
   mde_engine_io_desc(e, idx, &d);
   *rank = d.rank;
@@ -784,7 +673,7 @@ int mde_context_create(mde_engine* e, int max_batch, mde_context** out) {
     delete c;
     return hip_fail(he, "hipMalloc(activation arena)");
   }
-  plan_arena(*e, max_batch, &c->b, (uint8_t*)c->arena);
+  plan_arena(*e, max_batch, c, (uint8_t*)c->arena);
   // zero once: the q/k/v^T pad rows/columns beyond T must stay 0
   he = hipMemset(c->arena, 0, c->arena_bytes);
   if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking);
@@ -817,8 +706,10 @@ int mde_context_destroy(mde_context* c) {
 
 int mde_context_set_tensor_address(mde_context* c, const char* name, void* ptr) {
   if (int rc = check_ctx(c)) return rc;
-  if (is_input(c->e, name)) c->in = ptr;
-  else if (is_output(name)) c->out = ptr;
+  const int idx = io_index(c->e, name);
+  if (idx == 0) c->in = ptr;
+  else if (idx == 1) c->out = ptr;
+  else if (idx == 2) c->out2 = ptr;
   else return fail(MDE_ERR_NAME, std::string("unknown tensor ") + (name ? name : "(null)"));
   return MDE_OK;
 }
@@ -849,7 +740,7 @@ int mde_context_get_tensor_shape(const mde_context* c, const char* name, int64_t
   if (int rc = check_ctx(c)) return rc;
   if (!dims || !rank) return fail(MDE_ERR_ARG, "null argument");
   mde_io_desc d;
-  int idx = is_input(c->e, name) ? 0 : is_output(name) ? 1 : -1;
+  int idx = io_index(c->e, name);
   if (idx < 0) return fail(MDE_ERR_NAME, std::string("unknown tensor ") + (name ? name : "(null)"));
   mde_engine_io_desc(c->e, idx, &d);
   *rank = d.rank;
@@ -880,15 +771,19 @@ int mde_context_workspace_bytes(const mde_context* c, size_t* bytes) {
 
 int mde_context_enqueue(mde_context* c, void* stream) {
   if (int rc = check_ctx(c)) return rc;
-  if (!c->in || !c->out) return fail(MDE_ERR_STATE, "set_tensor_address('input'/'output') before enqueue");
+  if (!c->in || !c->out) return fail(MDE_ERR_STATE, "set_tensor_address(input / output) before enqueue");
+  int nio = 2;
+  mde_engine_num_io(c->e, &nio);
+  if (nio > 2 && !c->out2) return fail(MDE_ERR_STATE, "set_tensor_address('fov_deg') before enqueue");
   hipStream_t st = (hipStream_t)stream;
   HIP_OR(hipSetDevice(c->e->device), "hipSetDevice");
   const void* in = c->in;
   float* out = (float*)c->out;
+  float* out2 = (float*)c->out2;
   if (c->prof_cb) {
     c->prof_used = 0;
     Runner r{*c, st, true};
-    hipError_t he = r.forward(c->batch, in, out);
+    hipError_t he = run_forward(r, c->batch, in, out, out2);
     if (he != hipSuccess) return hip_fail(he, "enqueue (profiled)");
     HIP_OR(hipStreamSynchronize(st), "hipStreamSynchronize");
     for (size_t i = 0; i < c->prof_used; ++i) {
@@ -900,18 +795,18 @@ int mde_context_enqueue(mde_context* c, void* stream) {
   }
   if (!c->graph_mode) {
     Runner r{*c, st, false};
-    hipError_t he = r.forward(c->batch, in, out);
+    hipError_t he = run_forward(r, c->batch, in, out, out2);
     if (he != hipSuccess) return hip_fail(he, "enqueue");
     return MDE_OK;
   }
-  GraphKey key{c->batch, c->in, c->out};
+  GraphKey key{c->batch, c->in, c->out, c->out2};
   auto it = c->graphs.find(key);
   if (it == c->graphs.end()) {
     hipGraph_t g = nullptr;
     hipGraphExec_t ge = nullptr;
     HIP_OR(hipStreamBeginCapture(c->cap_stream, hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
     Runner r{*c, c->cap_stream, false};
-    hipError_t he = r.forward(c->batch, in, out);
+    hipError_t he = run_forward(r, c->batch, in, out, out2);
     hipError_t he2 = hipStreamEndCapture(c->cap_stream, &g);
     if (he != hipSuccess) {
       if (g) hipGraphDestroy(g);
@@ -1043,6 +938,37 @@ int mde_op_depth_postprocess(const float* depth, int batch, int ih, int iw, floa
   if (!depth || !out || batch < 1 || ih < 1 || iw < 1 || oh < 1 || ow < 1)
     return fail(MDE_ERR_ARG, "mde_op_depth_postprocess: bad argument");
   OP_RET(launch_depth_postprocess(depth, batch, ih, iw, out, oh, ow, lo, hi, (hipStream_t)st), "depth_postprocess");
+}
+
+int mde_op_dp_pyramid_patches(const float* img, int batch, int size, void* patches, void* st) {
+  if (!img || !patches || batch < 1 || size != 1536) return fail(MDE_ERR_ARG, "mde_op_dp_pyramid_patches: bad argument");
+  DpPyramid pyr;
+  pyr.nlev = 3;
+  const int f[3] = {1, 2, 4}, n[3] = {5, 3, 1}, stride[3] = {288, 192, 384};
+  int first = 0;
+  for (int i = 0; i < 3; ++i) {
+    pyr.first[i] = first;
+    pyr.n[i] = n[i];
+    pyr.stride[i] = stride[i];
+    pyr.f[i] = f[i];
+    first += n[i] * n[i];
+  }
+  pyr.nseq = first;
+  OP_RET(launch_dp_patch_prep(img, (h16*)patches, batch, size, 24, pyr, (hipStream_t)st), "dp_pyramid_patches");
+}
+
+int mde_op_merge_tokens(const float* x32, int batch, int tokens, int dim, int n, int g, int pad, int base,
+                        const float* gamma, const float* beta, float eps, void* out, void* st) {
+  if (!x32 || !out || batch < 1 || (gamma == nullptr) != (beta == nullptr))
+    return fail(MDE_ERR_ARG, "mde_op_merge_tokens: bad argument");
+  DpMerge m;
+  m.B = batch;
+  m.n = n;
+  m.G = g;
+  m.pad = pad;
+  m.base = base;
+  m.T = tokens;
+  OP_RET(launch_merge_tokens(x32, (h16*)out, gamma, beta, dim, m, eps, (hipStream_t)st), "merge_tokens");
 }
 
 int mde_op_layernorm(const float* x, void* y, const float* g, const float* b, int rows, int dim, float eps,

@@ -89,4 +89,26 @@ hipError_t launch_patch_prep(const float* img, h16* P, float* X, const float* cl
 hipError_t launch_resize(const h16* in, h16* out, int B, int ih, int iw, int C, int oh, int ow,
                          hipStream_t st);
 
+// ---- Depth Pro (depth_pro_ops.hip) ----
+// Pyramid levels of the patch encoder input, high-res first: sequences
+// l in [first[i], first[i+1]) are the n[i] x n[i] patches of level i
+// (row-major), taken with `stride` from the image downsampled by f[i].
+struct DpPyramid {
+  int nlev = 0, nseq = 0;  // nseq = patches per image
+  int first[3] = {0, 0, 0}, n[3] = {0, 0, 0}, stride[3] = {0, 0, 0}, f[3] = {1, 1, 1};
+};
+// One merged level map: patches (base + r*n + c) of every image, G x G
+// tokens each (row 0 of each sequence = cls, dropped), interior edges
+// trimmed by pad -> [B][n G - 2 (n-1) pad]^2 NHWC.
+struct DpMerge {
+  int B = 0, n = 1, G = 0, pad = 0, base = 0, T = 0;
+};
+hipError_t launch_dp_patch_prep(const float* img, h16* P, int B, int S, int G, const DpPyramid& pyr,
+                                hipStream_t st);
+hipError_t launch_cls_rows(float* X, const float* cls, int nseq, int T, int D, hipStream_t st);
+// g == nullptr: plain fp32 -> f16 copy (raw hook features); else LayerNorm(g, b)
+hipError_t launch_merge_tokens(const float* x, h16* y, const float* g, const float* b, int D, const DpMerge& m,
+                               float eps, hipStream_t st);
+hipError_t launch_fov_final(const h16* in, const float* w, float bias, int K, int B, float* out, hipStream_t st);
+
 }  // namespace mde

@@ -1,4 +1,4 @@
-// On-disk layout of a packed DA-V2 engine (written by pack.py, read by
+// On-disk layout of a packed engine (DA-V2 or Depth Pro) (written by pack.py, read by
 // engine.hip).  Little-endian, fixed-size records.
 //
 //   [0]            PackHeader   (32 B)
@@ -34,7 +34,14 @@ struct PackConfig {
   // engine computes ((float)u / in_scale - in_mean[c]) / in_std[c] in fp32
   int32_t input_u8;
   float in_scale, in_mean[3], in_std[3];
-  char reserved[128];
+  // model family (0 = Depth Anything V2, 1 = Depth Pro) and the Depth Pro
+  // decoder geometry (HF DepthProConfig fields; zero for DA-V2).  For Depth
+  // Pro, img_h/img_w = the fixed 1536 input, patch = 16, vit_size = 384,
+  // features = fusion_hidden_size, metric = 0 (ReLU head).
+  int32_t family;
+  int32_t vit_size, merge_pad, use_fov, fov_layers, fov_k;
+  int32_t hooks[2], inter_dims[2], scaled_dims[3];
+  char reserved[76];
 };
 static_assert(sizeof(PackConfig) == 256, "PackConfig");
 

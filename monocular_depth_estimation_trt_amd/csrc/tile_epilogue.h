@@ -42,7 +42,7 @@ MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&m
       if (n >= p.N) continue;
       float4 bn = {0.f, 0.f, 0.f, 0.f};
       if constexpr (EM == E_CONVT) {
-        bn = *reinterpret_cast<const float4*>(p.bias + (n % p.cout));
+        if (p.bias) bn = *reinterpret_cast<const float4*>(p.bias + (n % p.cout));
       } else {
         if (p.bias) bn = *reinterpret_cast<const float4*>(p.bias + n);
       }

@@ -201,9 +201,9 @@ def _config_bytes(cfg: dict, img_h: int, img_w: int, input_format: str = "float3
     return b + b"\0" * 128
 
 
-def pack_bytes(sd: Dict[str, np.ndarray], cfg: dict, img_h: int = 518, img_w: int = 518,
-               input_format: str = "float32_nchw") -> bytes:
-    tens = packed_tensors(sd, cfg, img_h, img_w)
+def container(tens: "OrderedDict[str, np.ndarray]", cfg_bytes: bytes) -> bytes:
+    """Header + PackConfig + tensor table + 256-byte aligned data."""
+    assert len(cfg_bytes) == 256, len(cfg_bytes)
     n = len(tens)
     table = bytearray()
     data = bytearray()
@@ -221,9 +221,14 @@ def pack_bytes(sd: Dict[str, np.ndarray], cfg: dict, img_h: int = 518, img_w: in
     head_len = 32 + 256 + len(table)
     data_offset = -(-head_len // ALIGN) * ALIGN
     header = struct.pack("<8sIIQQ", b"MDEPACK1", PACK_VERSION, n, data_offset, len(data))
-    blob = header + _config_bytes(cfg, img_h, img_w, input_format) + bytes(table)
+    blob = header + cfg_bytes + bytes(table)
     blob += b"\0" * (data_offset - len(blob))
     return blob + bytes(data)
+
+
+def pack_bytes(sd: Dict[str, np.ndarray], cfg: dict, img_h: int = 518, img_w: int = 518,
+               input_format: str = "float32_nchw") -> bytes:
+    return container(packed_tensors(sd, cfg, img_h, img_w), _config_bytes(cfg, img_h, img_w, input_format))
 
 
 def write_packed(path: str, blob: bytes) -> str:

@@ -55,3 +55,26 @@ class DevicePostprocess:
     def __exit__(self, *exc):
         self.free()
         return False
+
+
+def depth_pro_postprocess(canonical_inverse_depth: np.ndarray, fov_deg: np.ndarray, src_hw, f_px=None):
+    """Reference `models/depth_pro/onnx2trt.py:100-117` (outside its timed
+    loop): focal length from the predicted FOV (unless given), inverse depth
+    rescaled by W / f_px, bilinear (align_corners=False) to the source size
+    when it differs from the engine's, depth = 1 / clamp(inv, 1e-4, 1e4).
+    Returns (depth [H, W] float32, f_px float)."""
+    import torch
+    import torch.nn.functional as F
+    inv = torch.from_numpy(np.ascontiguousarray(canonical_inverse_depth, dtype=np.float32)).reshape(
+        1, 1, *canonical_inverse_depth.shape[-2:])
+    H, W = int(src_hw[0]), int(src_hw[1])
+    if f_px is None:
+        fov = torch.from_numpy(np.asarray(fov_deg, dtype=np.float32).reshape(-1)[:1])
+        f_px = 0.5 * W / torch.tan(0.5 * torch.deg2rad(fov.to(torch.float)))
+    else:
+        f_px = torch.tensor([float(f_px)])
+    inv = inv * (W / f_px)
+    if (H, W) != tuple(inv.shape[-2:]):
+        inv = F.interpolate(inv, size=(H, W), mode="bilinear", align_corners=False)
+    depth = 1.0 / torch.clamp(inv, min=1e-4, max=1e4)
+    return depth.squeeze().numpy(), float(f_px.squeeze())

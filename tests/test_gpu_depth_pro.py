@@ -1,0 +1,143 @@
+"""Depth Pro on the HIP engine, through the C ABI,
+against the oracle (oracle/depth_pro_ref.py, HF-pinned by
+tests/golden/make_golden_depth_pro.py) on the "tiny" preset: the full
+1536x1536 geometry -- 35 pyramid patches, 24x24 tokens, the merge trims, five
+fusion levels, the 1536^2 head and the FOV head -- with narrow layers so the
+CPU oracle runs in seconds.
+
+Tolerance (fp16 operands, fp32 accumulation vs the fp32 oracle), stated
+here: canonical inverse depth rel_mean <= 1 %, Pearson corr >= 0.999,
+per pixel |d - d_ref| <= 3 % of the map's max; FOV |deg - ref| <= 2e-2 + 1 %.
+The kernels with no arithmetic freedom (pyramid patch gather, token merge)
+are held to f16 rounding of the fp32 reference.
+"""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from gpu_util import depth_metrics, op, ptr, stream
+
+from monocular_depth_estimation_trt_amd import pack_depth_pro, weights_depth_pro as WD
+from monocular_depth_estimation_trt_amd.engine import Engine
+from oracle import depth_pro_ref
+
+pytestmark = pytest.mark.gpu
+
+
+def _cfg():
+    return WD.depth_pro_config("tiny")
+
+
+def run_engine(blob, x: np.ndarray, graph=True):
+    B = x.shape[0]
+    eng = Engine.from_bytes(blob, 0, profile=((1,) + x.shape[1:], (B,) + x.shape[1:], (B,) + x.shape[1:]))
+    assert [eng.get_tensor_name(i) for i in range(eng.num_io_tensors)] == \
+        ["input", "canonical_inverse_depth", "fov_deg"]
+    ctx = eng.create_execution_context()
+    ctx.set_graph_mode(graph)
+    xin = torch.from_numpy(x).cuda()
+    out = torch.full((B, 1, x.shape[2], x.shape[3]), float("nan"), device="cuda")
+    fov = torch.full((B,), float("nan"), device="cuda")
+    ctx.set_input_shape("input", x.shape)
+    ctx.set_tensor_address("input", xin.data_ptr())
+    ctx.set_tensor_address("canonical_inverse_depth", out.data_ptr())
+    ctx.set_tensor_address("fov_deg", fov.data_ptr())
+    ctx.execute_async_v3(torch.cuda.current_stream().cuda_stream)
+    torch.cuda.synchronize()
+    y, f = out.cpu().numpy()[:, 0], fov.cpu().numpy()
+    ctx.destroy()
+    eng.destroy()
+    return y, f
+
+
+@pytest.fixture(scope="module")
+def tiny_case(gpu):
+    cfg = _cfg()
+    sd = WD.synthetic_state_dict(cfg, 4321)
+    x = WD.synthetic_images(2, cfg["img"], first_seed=200)
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    ref, fov_ref = depth_pro_ref.forward(depth_pro_ref.to_torch(sd), cfg, x)
+    return cfg, sd, x, ref.numpy(), fov_ref.numpy(), pack_depth_pro.pack_bytes(sd, cfg)
+
+
+def test_pyramid_patches_op(gpu):
+    cfg = _cfg()
+    x = torch.from_numpy(WD.synthetic_images(2, cfg["img"], first_seed=7))
+    pt, counts = depth_pro_ref.pyramid_patches(x, cfg)                       # [35B, 3, 384, 384]
+    N = pt.shape[0]
+    rows = pt.reshape(N, 3, 24, 16, 24, 16).permute(0, 2, 4, 1, 3, 5).reshape(N * 576, 768)
+    out = torch.empty(N * 576, 768, dtype=torch.float16, device="cuda")
+    op("mde_op_dp_pyramid_patches", ptr(x.cuda()), 2, cfg["img"], ptr(out), stream())
+    err = (out.float().cpu() - rows).abs()
+    assert counts == [2, 18, 50]
+    assert float(err.max()) <= 1e-3, float(err.max())   # |x| <= 1: f16 rounding only
+
+
+@pytest.mark.parametrize("ln", [False, True])
+@pytest.mark.parametrize("level", [0, 1, 2])
+def test_merge_tokens_op(gpu, ln, level):
+    """merge of the high (5x5, pad 3), med (3x3, pad 6) and low (1 patch) levels."""
+    B, G, D, T = 2, 24, 128, 577
+    n, pad, base = [(5, 3, 0), (3, 6, 25), (1, 0, 34)][level]
+    torch.manual_seed(level)
+    X = torch.randn(35 * B, T, D) * 2 + 0.5
+    g = 1 + 0.1 * torch.randn(D)
+    b = 0.1 * torch.randn(D)
+    src = torch.nn.functional.layer_norm(X, (D,), g, b, 1e-6) if ln else X
+    maps = depth_pro_ref._grid(src[base * B:(base + n * n) * B])           # [n*n*B, D, G, G]
+    ref = depth_pro_ref.merge(maps, B, pad).permute(0, 2, 3, 1)             # NHWC
+    side = n * G - 2 * (n - 1) * pad
+    out = torch.empty(B, side, side, D, dtype=torch.float16, device="cuda")
+    op("mde_op_merge_tokens", ptr(X.cuda()), B, T, D, n, G, pad, base,
+       ptr(g.cuda() if ln else None), ptr(b.cuda() if ln else None), 1e-6, ptr(out), stream())
+    assert ref.shape == out.shape
+    err = (out.float().cpu() - ref).abs()
+    assert float(err.max()) <= 2e-3 * float(ref.abs().max()) + 1e-3, float(err.max())
+
+
+def test_engine_matches_oracle(tiny_case):
+    cfg, sd, x, ref, fov_ref, blob = tiny_case
+    y, fov = run_engine(blob, x)
+    assert y.shape == ref.shape == (2, 1536, 1536)
+    m = depth_metrics(y, ref)
+    print("depth_pro tiny B=2", m, "fov", fov, fov_ref)
+    assert np.isfinite(y).all() and np.isfinite(fov).all()
+    assert m["rel_mean"] <= 1e-2, m
+    assert m["corr"] >= 0.999, m
+    assert m["max_abs"] <= 0.03 * float(np.abs(ref).max()), m
+    assert np.all(np.abs(fov - fov_ref) <= 2e-2 + 1e-2 * np.abs(fov_ref)), (fov, fov_ref)
+
+
+def test_engine_matches_hf_golden(tiny_case):
+    cfg, sd, x, ref, fov_ref, blob = tiny_case
+    z = np.load(os.path.join(GOLDEN, "depth_pro_tiny_b2.npz"), allow_pickle=False)
+    assert WD.state_dict_digest(sd) == str(z["weights_sha256"])
+    y, fov = run_engine(blob, x)
+    m = depth_metrics(y[:, ::8, ::8], z["output_hf_sub8"])
+    assert m["rel_mean"] <= 1e-2 and m["corr"] >= 0.999, m
+    assert np.all(np.abs(fov - z["fov_hf"]) <= 2e-2 + 1e-2 * np.abs(z["fov_hf"])), (fov, z["fov_hf"])
+
+
+def test_graph_equals_eager_and_batch_consistency(tiny_case):
+    cfg, sd, x, ref, fov_ref, blob = tiny_case
+    yg, fg = run_engine(blob, x, graph=True)
+    ye, fe = run_engine(blob, x, graph=False)
+    assert np.array_equal(yg, ye) and np.array_equal(fg, fe)
+    y1, f1 = run_engine(blob, x[1:2])   # image 1 alone == image 1 of the batch
+    assert np.array_equal(y1[0], yg[1]) and np.array_equal(f1[0], fg[1])
+
+
+def test_engine_rejects_bad_shapes(tiny_case):
+    cfg, sd, x, ref, fov_ref, blob = tiny_case
+    eng = Engine.from_bytes(blob, 0, profile=((1, 3, 1536, 1536),) * 3)
+    ctx = eng.create_execution_context()
+    with pytest.raises(RuntimeError):
+        ctx.set_input_shape("input", (1, 3, 1024, 1024))
+    with pytest.raises(RuntimeError):
+        ctx.set_tensor_address("output", 0)   # DA-V2's name: not a Depth Pro binding
+    ctx.destroy()
+    eng.destroy()
