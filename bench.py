@@ -2,6 +2,7 @@
 """Depth Anything V2 throughput on MI355X through the HIP engine.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--encoder vits]
+    python bench.py --model depth_pro [--batch 4]     (SURVEY.md 8f row 3, 1536^2)
 
 One *step* = one forward of the packed DA-V2 engine over one batch of B
 synthetic 518x518 images already resident in HBM (input fp32 NCHW, output
@@ -45,6 +46,7 @@ MFMA_PEAK_TFLOPS = 2500.0   # dense fp16/bf16 MFMA, MI355X (MI355X_MICROARCH.md 
 ENC_LABEL = {"vits": "ViT-S", "vitb": "ViT-B", "vitl": "ViT-L"}
 REF_B1_FPS = 232.11         # RTX 3080 TRT fp16, BASELINE.md
 REF_B1_U8_FPS = 294.07      # same, uint8-NHWC input engine (reports/uint8_ab/depth_anything_v2.json)
+REF_DP_B1_FPS = 4.13        # Depth Pro 1536^2 TRT fp16, RTX 3080 (242.12 ms, BASELINE.md / SURVEY.md 6)
 
 
 def log(*a):
@@ -56,7 +58,8 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--batch", type=int, default=32, help="images per GPU per step")
+    p.add_argument("--model", default="depth_anything_v2", choices=["depth_anything_v2", "depth_pro"])
+    p.add_argument("--batch", type=int, default=0, help="images per GPU per step (default 32; depth_pro 4)")
     p.add_argument("--encoder", default="vits", choices=["vits", "vitb", "vitl"])
     p.add_argument("--size", type=int, default=518)
     p.add_argument("--b1-iters", type=int, default=100)
@@ -115,8 +118,12 @@ def pmc_traffic(cls, cfg, B, size):
 
 
 def roofline(cfg, B, size, layer_ms):
-    from monocular_depth_estimation_trt_amd import flops
-    lf = flops.layer_flops(cfg, size, size, B)
+    if cfg.get("family") == "depth_pro":
+        from monocular_depth_estimation_trt_amd import flops_depth_pro as flops
+        lf = flops.layer_flops(cfg, B)
+    else:
+        from monocular_depth_estimation_trt_amd import flops
+        lf = flops.layer_flops(cfg, size, size, B)
     cls_ms, cls_fl, cls_n = {}, {}, {}
     for name, ms in layer_ms.items():
         c = flops.layer_class(name)
@@ -130,7 +137,7 @@ def roofline(cfg, B, size, layer_ms):
     breakdown = {c: {"ms": round(cls_ms[c], 4), "launches": cls_n[c],
                      "tflops": round(cls_fl[c] / (cls_ms[c] * 1e-3) / 1e12, 1) if cls_fl.get(c) else None}
                  for c in sorted(cls_ms, key=lambda c: -cls_ms[c])}
-    traffic, src = pmc_traffic(dom, cfg, B, size)
+    traffic, src = pmc_traffic(dom, cfg, B, size) if cfg.get("family") != "depth_pro" else (None, None)
     roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
             "flop_per_launch": per_launch_fl, "avg_launch_ms": round(avg_ms, 5),
@@ -141,17 +148,18 @@ def roofline(cfg, B, size, layer_ms):
     return roof, breakdown
 
 
-def b1_reference_method(blob, dev, size, warmup, iters, u8=False, prefix="b1_"):
-    """Batch-1 wall clock exactly as core/bench.py measures the TRT engine.
-    u8: the uint8-NHWC engine (the reference's A/B, reports/uint8_ab/
-    depth_anything_v2.json: 294.07 FPS on the 3080), 0.8 MB H2D."""
+def b1_reference_method(blob, dev, images, warmup, iters, ref_fps, prefix="b1_"):
+    """Batch-1 wall clock exactly as core/bench.py measures the TRT engine:
+    pinned H2D of `images` (one image), enqueue, D2H of every output, sync;
+    20 warmup / 100 iterations, StageTimer split.  For the DA-V2 uint8-NHWC
+    engine (the reference's A/B, reports/uint8_ab/depth_anything_v2.json:
+    294.07 FPS on the 3080) the H2D is 0.8 MB."""
     from monocular_depth_estimation_trt_amd import common_runtime as cr
-    from monocular_depth_estimation_trt_amd import weights
     from monocular_depth_estimation_trt_amd.engine import Engine
     eng = Engine.from_bytes(blob, dev)
     ctx = eng.create_execution_context()
     inputs, outputs, bindings, stream = cr.allocate_buffers(eng, None, profile_idx=0)
-    inputs[0].host = (weights.synthetic_images_u8 if u8 else weights.synthetic_images)(1, size, size, first_seed=0)
+    inputs[0].host = images
     timer = cr.StageTimer()
     fn = lambda: cr.do_inference(ctx, eng, bindings, inputs, outputs, stream, timer=timer)  # noqa: E731
     for _ in range(warmup):
@@ -171,33 +179,100 @@ def b1_reference_method(blob, dev, size, warmup, iters, u8=False, prefix="b1_"):
     mean = statistics.fmean(samples)
     s = sorted(samples)
     pct = lambda q: s[min(len(s) - 1, max(0, int(np.ceil(q / 100 * len(s))) - 1))]  # noqa: E731
-    ref = REF_B1_U8_FPS if u8 else REF_B1_FPS
     res = {"mean_ms": round(mean, 4), "p50_ms": round(pct(50), 4), "p99_ms": round(pct(99), 4),
-           "fps": round(1000.0 / mean, 2), "vs_ref_fps": round(1000.0 / mean / ref, 3)}
+           "fps": round(1000.0 / mean, 2), "vs_ref_fps": round(1000.0 / mean / ref_fps, 3)}
     for k, v in stages.items():
         res[k] = round(statistics.fmean(v), 4)
     res["out_mean"] = float(out.mean())
     return {prefix + k: v for k, v in res.items()}
 
 
-def cpu_baseline(cfg, size, seconds):
-    import torch
-    from oracle import dav2_ref
-    from monocular_depth_estimation_trt_amd import weights
-    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
-    w = dav2_ref.to_torch(weights.synthetic_state_dict(cfg, 1234))
-    x = torch.from_numpy(weights.synthetic_images(1, size, size, first_seed=0))
-    dav2_ref.forward(w, cfg, x)   # warmup
+def _timed_cpu(fn, seconds, warmup=True, max_n=200):
+    if warmup:
+        fn()
     n, t0 = 0, time.perf_counter()
     while True:
-        dav2_ref.forward(w, cfg, x)
+        fn()
         n += 1
         el = time.perf_counter() - t0
-        if el >= seconds or n >= 200:
-            break
+        if el >= seconds or n >= max_n:
+            return n, el
+
+
+def cpu_baseline(cfg, size, seconds):
+    import torch
+    torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
+    if cfg.get("family") == "depth_pro":
+        # one full fp32 forward is ~19 TFLOP: the sample is ONE forward, no warmup
+        from oracle import depth_pro_ref
+        from monocular_depth_estimation_trt_amd import weights_depth_pro as WD
+        w = depth_pro_ref.to_torch(WD.synthetic_state_dict(cfg, 4321))
+        x = torch.from_numpy(WD.synthetic_images(1, size, first_seed=0))
+        n, el = _timed_cpu(lambda: depth_pro_ref.forward(w, cfg, x), seconds, warmup=False, max_n=1)
+        what = f"{n} x Depth Pro {size}x{size} batch-1 fp32 forward of oracle/depth_pro_ref.py (torch CPU), no warmup"
+    else:
+        from oracle import dav2_ref
+        from monocular_depth_estimation_trt_amd import weights
+        w = dav2_ref.to_torch(weights.synthetic_state_dict(cfg, 1234))
+        x = torch.from_numpy(weights.synthetic_images(1, size, size, first_seed=0))
+        n, el = _timed_cpu(lambda: dav2_ref.forward(w, cfg, x), seconds)
+        what = (f"{n} x DA-V2 {cfg['encoder']} {size}x{size} batch-1 fp32 forwards of oracle/dav2_ref.py "
+                f"(torch CPU) after 1 warmup")
     return {"value": round(n / el, 3), "unit": "images/s", "cores": torch.get_num_threads(), "kind": "port",
-            "sample": f"{n} x DA-V2 {cfg['encoder']} {size}x{size} batch-1 fp32 forwards of oracle/dav2_ref.py "
-                      f"(torch CPU) after 1 warmup, {el:.1f} s"}
+            "sample": f"{what}, {el:.1f} s"}
+
+
+class Workload:
+    """The packed engine, its io tensors and the constants of one bench model."""
+
+    def __init__(self, a, rank):
+        import torch
+        if a.model == "depth_pro":
+            from monocular_depth_estimation_trt_amd import pack_depth_pro as PD
+            from monocular_depth_estimation_trt_amd import weights_depth_pro as WD
+            from monocular_depth_estimation_trt_amd.flops_depth_pro import total_flops
+            self.cfg = WD.depth_pro_config("dinov2l16_384")
+            self.S = S = self.cfg["img"]
+            self.B = B = a.batch or 4
+            self.sd = WD.synthetic_state_dict(self.cfg, 4321)
+            self.blob = PD.pack_bytes(self.sd, self.cfg)
+            self.images = lambda n, seed: WD.synthetic_images(n, S, first_seed=seed)  # noqa: E731
+            self.outs = {"canonical_inverse_depth": (B, 1, S, S), "fov_deg": (B,)}
+            self.gflop = total_flops(self.cfg) / 1e9
+            self.ref_fps = REF_DP_B1_FPS
+            self.label = "Depth Pro"
+            self.workload = (f"Depth Pro (3 x DINOv2-L/16 at 384^2, 35-patch pyramid, FOV head) {S}x{S}, forward, "
+                             f"batch {B} per GPU, inputs resident in HBM, hipGraph replay")
+            self.weights = "synthetic seeded (seed 4321), fan-in scaled"
+            self.encoder = "dinov2l16_384"
+        else:
+            from monocular_depth_estimation_trt_amd import pack, weights
+            from monocular_depth_estimation_trt_amd.flops import total_flops
+            self.S = S = a.size
+            self.B = B = a.batch or 32
+            self.cfg = weights.model_config(a.encoder, "metric")
+            self.sd = weights.synthetic_state_dict(self.cfg, 1234)
+            self.blob = pack.pack_bytes(self.sd, self.cfg, S, S)
+            self.images = lambda n, seed: weights.synthetic_images(n, S, S, first_seed=seed)  # noqa: E731
+            self.outs = {"output": (B, S, S)}
+            self.gflop = total_flops(self.cfg, S, S) / 1e9
+            self.ref_fps = REF_B1_FPS
+            self.label = f"DA-V2 {ENC_LABEL.get(a.encoder, a.encoder)}"
+            self.workload = (f"Depth Anything V2 {a.encoder} {S}x{S} metric head, forward, batch {B} per GPU, "
+                             f"inputs resident in HBM, hipGraph replay")
+            self.weights = "synthetic seeded (seed 1234), fan-in scaled"
+            self.encoder = a.encoder
+        self.x = torch.from_numpy(self.images(self.B, rank * self.B)).cuda()
+        self.y = {k: torch.empty(v, device="cuda") for k, v in self.outs.items()}
+
+    def b1_legs(self, a, dev):
+        res = b1_reference_method(self.blob, dev, self.images(1, 0), a.b1_warmup, a.b1_iters, self.ref_fps)
+        if a.model == "depth_anything_v2":
+            from monocular_depth_estimation_trt_amd import pack, weights
+            blob_u8 = pack.pack_bytes(self.sd, self.cfg, self.S, self.S, input_format="uint8_nhwc")
+            res.update(b1_reference_method(blob_u8, dev, weights.synthetic_images_u8(1, self.S, self.S, first_seed=0),
+                                           a.b1_warmup, a.b1_iters, REF_B1_U8_FPS, prefix="b1_u8_"))
+        return res
 
 
 def main():
@@ -216,21 +291,17 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(local)
 
-    from monocular_depth_estimation_trt_amd import pack, weights
     from monocular_depth_estimation_trt_amd.engine import Engine
-    from monocular_depth_estimation_trt_amd.flops import total_flops
 
-    B, S = a.batch, a.size
-    cfg = weights.model_config(a.encoder, "metric")
-    sd = weights.synthetic_state_dict(cfg, 1234)
-    blob = pack.pack_bytes(sd, cfg, S, S)
-    eng = Engine.from_bytes(blob, local, profile=((1, 3, S, S), (B, 3, S, S), (B, 3, S, S)))
+    wl = Workload(a, rank)
+    B, S = wl.B, wl.S
+    shape = tuple(wl.x.shape)
+    eng = Engine.from_bytes(wl.blob, local, profile=((1,) + shape[1:], shape, shape))
     ctx = eng.create_execution_context()
-    x = torch.from_numpy(weights.synthetic_images(B, S, S, first_seed=rank * B)).cuda()
-    y = torch.empty(B, S, S, device="cuda")
-    ctx.set_input_shape("input", (B, 3, S, S))
-    ctx.set_tensor_address("input", x.data_ptr())
-    ctx.set_tensor_address("output", y.data_ptr())
+    ctx.set_input_shape("input", shape)
+    ctx.set_tensor_address("input", wl.x.data_ptr())
+    for k, t in wl.y.items():
+        ctx.set_tensor_address(k, t.data_ptr())
     st = torch.cuda.Stream()
     sh = st.cuda_stream
 
@@ -241,7 +312,7 @@ def main():
     el = replicas.timed_region(lambda: ctx.execute_async_v3(sh), a.steps, torch.cuda.synchronize,
                                dist.barrier if dist is not None else None)
     el = replicas.max_over_ranks(el)
-    out_ok = bool(torch.isfinite(y).all().item())
+    out_ok = all(bool(torch.isfinite(t).all().item()) for t in wl.y.values())
     value = world * B * a.steps / el
     ms_step = el / a.steps * 1e3
 
@@ -252,34 +323,28 @@ def main():
         return
 
     layer_ms = profile_layers(ctx, sh, a.profile_iters)
-    roof, breakdown = roofline(cfg, B, S, layer_ms)
+    roof, breakdown = roofline(wl.cfg, B, S, layer_ms)
     if a.layers_json:
         with open(a.layers_json, "w") as f:
             json.dump({"batch": B, "layer_ms": layer_ms, "classes": breakdown, "roofline": roof}, f, indent=1)
-    gflop = total_flops(cfg, S, S) / 1e9
-    model_frac = value / world * gflop * 1e9 / (MFMA_PEAK_TFLOPS * 1e12)
-    res_b1 = {} if a.no_b1 else b1_reference_method(blob, local, S, a.b1_warmup, a.b1_iters)
-    if not a.no_b1:
-        blob_u8 = pack.pack_bytes(sd, cfg, S, S, input_format="uint8_nhwc")
-        res_b1.update(b1_reference_method(blob_u8, local, S, a.b1_warmup, a.b1_iters, u8=True, prefix="b1_u8_"))
+    model_frac = value / world * wl.gflop * 1e9 / (MFMA_PEAK_TFLOPS * 1e12)
     ctx.destroy()
     eng.destroy()
+    res_b1 = {} if a.no_b1 else wl.b1_legs(a, local)
     cpu = None
     if world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(cfg, S, a.cpu_seconds)
-    for c, v in list(breakdown.items())[:8]:
+        cpu = cpu_baseline(wl.cfg, S, a.cpu_seconds)
+    for c, v in list(breakdown.items())[:10]:
         log(f"{c:24s} {v['ms']:9.4f} ms  x{v['launches']:3d}  {v['tflops']} TF/s")
     line = {
-        "metric": f"depth FPS (images/s) at {S}x{S} fp16, DA-V2 {ENC_LABEL.get(a.encoder, a.encoder)}, MI355X",
+        "metric": f"depth FPS (images/s) at {S}x{S} fp16, {wl.label}, MI355X",
         "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": round(value / REF_B1_FPS, 3), "dtype": "fp16", "data": "synthetic",
-        "config": {"workload": f"Depth Anything V2 {a.encoder} {S}x{S} metric head, forward, batch {B} per GPU, "
-                               f"inputs resident in HBM, hipGraph replay",
-                   "encoder": a.encoder, "img": [S, S], "batch_per_gpu": B, "global_batch": B * world,
-                   "parallelism": f"replica x{world} (batch shards, no collectives)",
-                   "weights": "synthetic seeded (seed 1234), fan-in scaled"},
-        "model_gflop_per_image": round(gflop, 2),
+        "vs_baseline": round(value / wl.ref_fps, 3), "dtype": "fp16", "data": "synthetic",
+        "config": {"workload": wl.workload, "encoder": wl.encoder, "img": [S, S], "batch_per_gpu": B,
+                   "global_batch": B * world, "parallelism": f"replica x{world} (batch shards, no collectives)",
+                   "weights": wl.weights},
+        "model_gflop_per_image": round(wl.gflop, 2),
         "model_mfma_frac": round(model_frac, 4),
         "roofline": roof,
         "cpu_baseline": cpu,
