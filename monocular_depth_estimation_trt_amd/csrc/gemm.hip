@@ -29,6 +29,7 @@
 //    output columns of one row: the fused epilogue (tile_epilogue.h) stores
 //    8 B (f16) / 16 B (f32) per lane straight from the accumulators.
 #include <cstdlib>
+#include <cstring>
 
 #include "mde_device.h"
 #include "mde_ops.h"
@@ -442,15 +443,17 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) 
     if (z == z) return;
   }
 #endif
-#if MDE_EPI_LDS
-  static_assert(BM * BN * 4 <= SG * STAGE, "LDS-staged epilogue slices");
-  if constexpr (SG > 2) lds_barrier();  // the ring's last stage may still be read by other waves
-  const int m0w = m0 + wm * TM * 16;
-  if (!store_tile_lds<EM, TM, TN>(
-          p, acc, [&](int row) { return m0w + row < p.M ? m0w + row : -1; }, n0 + wn * TN * 16, lane,
-          smem + wave * (TM * 16) * (TN * 16) * 4))
-#endif
-    store_tile<EM, TM, TN>(p, acc, mrow, n0 + wn * TN * 16 + (lane >> 4) * 4, lane);
+  // LDS-staged epilogue when every wave's fp32 tile fits in the ring
+  constexpr bool EPI_LDS = MDE_EPI_LDS && BM * BN * 4 <= SG * STAGE;
+  bool staged = false;
+  if constexpr (EPI_LDS) {
+    if constexpr (SG > 2) lds_barrier();  // the ring's last stage may still be read by other waves
+    const int m0w = m0 + wm * TM * 16;
+    staged = store_tile_lds<EM, TM, TN>(
+        p, acc, [&](int row) { return m0w + row < p.M ? m0w + row : -1; }, n0 + wn * TN * 16, lane,
+        smem + wave * (TM * 16) * (TN * 16) * 4);
+  }
+  if (!staged) store_tile<EM, TM, TN>(p, acc, mrow, n0 + wn * TN * 16 + (lane >> 4) * 4, lane);
   if constexpr (EM == E_RESID) {
     if (p.ln_counter) ln_tail<NW>(p, tm, m0, BM, ntn, smem, tid);
   }
@@ -466,8 +469,32 @@ hipError_t run(const GemmParams& p, hipStream_t st) {
   return hipGetLastError();
 }
 
+// tuning override for large dense problems: MDE_GEMM_TILE = 256x256 | 256x128 | 128x256
+int tile_override() {
+  static const int v = [] {
+    const char* e = getenv("MDE_GEMM_TILE");
+    if (!e) return 0;
+    if (!strcmp(e, "256x256")) return 1;
+    if (!strcmp(e, "256x128")) return 2;
+    if (!strcmp(e, "128x256")) return 3;
+    return 0;
+  }();
+  return v;
+}
+
 template <int AM, int EM>
 hipError_t dispatch(const GemmParams& p, hipStream_t st) {
+  if constexpr (AM == A_DENSE && EM != E_HEAD) {
+    const long long t256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256);
+    if (t256 >= 512) {
+      switch (tile_override()) {
+        case 1: return run<256, 256, 2, 2, AM, EM>(p, st);
+        case 2: return run<256, 128, 2, 2, AM, EM>(p, st);
+        case 3: return run<128, 256, 2, 2, AM, EM>(p, st);
+        default: break;
+      }
+    }
+  }
   if constexpr (EM == E_HEAD) {
     return run<128, 32, 4, 1, AM, EM>(p, st);
   } else {
@@ -507,6 +534,7 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
   if (p.amode != A_DENSE && conv_direct_supported(p) && !getenv_im2col()) return launch_conv3(p, st);
   if (p.ln_counter && (p.emode != E_RESID || (p.N != 384 && p.N != 768 && p.N != 1024) || p.ldo != p.N))
     return hipErrorInvalidValue;
+  if (gemm256_eligible(p)) return launch_gemm256(p, st);
   if (p.amode == A_DENSE && gemm_persistent_enabled() && !p.ln_counter) {
     // one 256x128 tile per CU per round at least: the persistent pipeline wins
     const long long tiles = (long long)((p.M + 255) / 256) * ((p.N + 127) / 128);

@@ -70,6 +70,10 @@ hipError_t launch_conv3(const GemmParams& p, hipStream_t st);
 // Persistent pipelined dense GEMM (gemm_persistent.hip); launch_gemm routes
 // large dense problems here when MDE_GEMM_PERSISTENT=1 (A/B tuning path).
 bool gemm_persistent_enabled();
+// 256x256 phase-pipelined dense GEMM (gemm256.hip) for large token-major
+// problems; launch_gemm routes there when gemm256_eligible() (MDE_GEMM256=0 off).
+bool gemm256_eligible(const GemmParams& p);
+hipError_t launch_gemm256(const GemmParams& p, hipStream_t st);
 hipError_t launch_gemm_persistent(const GemmParams& p, hipStream_t st);
 
 hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T,
