@@ -3,6 +3,7 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--encoder vits]
     python bench.py --model depth_pro [--batch 4]     (SURVEY.md 8f row 3, 1536^2)
+    python bench.py --model vggt [--batch 8] [--frames 1]   (SURVEY.md 8f row 4, 518^2)
 
 One *step* = one forward of the packed DA-V2 engine over one batch of B
 synthetic 518x518 images already resident in HBM (input fp32 NCHW, output
@@ -11,7 +12,8 @@ captured hipGraph.  N > 1: one process per GPU (torch.distributed.run),
 each rank an independent replica on its own batch shard -- no collective on
 the data path; a gloo barrier brackets the timed region and
 the max time over ranks is used.  `value` = images processed by all ranks /
-that time (weak scaling: per-GPU batch fixed).
+that time (weak scaling: per-GPU batch fixed).  VGGT counts frames: a batch
+item of S frames is S images.
 
 Also measured (rank 0):
   * b1_*: the reference's own methodology (core/bench.py:182-210): batch 1,
@@ -47,6 +49,7 @@ ENC_LABEL = {"vits": "ViT-S", "vitb": "ViT-B", "vitl": "ViT-L"}
 REF_B1_FPS = 232.11         # RTX 3080 TRT fp16, BASELINE.md
 REF_B1_U8_FPS = 294.07      # same, uint8-NHWC input engine (reports/uint8_ab/depth_anything_v2.json)
 REF_DP_B1_FPS = 4.13        # Depth Pro 1536^2 TRT fp16, RTX 3080 (242.12 ms, BASELINE.md / SURVEY.md 6)
+REF_VGGT_B1_FPS = 19.02     # VGGT 518^2 S=1 TRT fp16, RTX 3080 (52.58 ms, BASELINE.md / SURVEY.md 6)
 
 
 def log(*a):
@@ -58,8 +61,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
-    p.add_argument("--model", default="depth_anything_v2", choices=["depth_anything_v2", "depth_pro"])
-    p.add_argument("--batch", type=int, default=0, help="images per GPU per step (default 32; depth_pro 4)")
+    p.add_argument("--model", default="depth_anything_v2", choices=["depth_anything_v2", "depth_pro", "vggt"])
+    p.add_argument("--batch", type=int, default=0,
+                   help="batch items per GPU per step (default 32; depth_pro 4; vggt 8)")
+    p.add_argument("--frames", type=int, default=1, help="vggt: frames per batch item (the packed S)")
     p.add_argument("--encoder", default="vits", choices=["vits", "vitb", "vitl"])
     p.add_argument("--size", type=int, default=518)
     p.add_argument("--b1-iters", type=int, default=100)
@@ -117,13 +122,21 @@ def pmc_traffic(cls, cfg, B, size):
     return None, None
 
 
-def roofline(cfg, B, size, layer_ms):
-    if cfg.get("family") == "depth_pro":
+def roofline(cfg, B, size, layer_ms, frames=1):
+    fam = cfg.get("family")
+    if fam == "depth_pro":
         from monocular_depth_estimation_trt_amd import flops_depth_pro as flops
         lf = flops.layer_flops(cfg, B)
+    elif fam == "vggt":
+        from monocular_depth_estimation_trt_amd import flops_vggt as flops
+        lf = flops.layer_flops(cfg, B, frames)
     else:
         from monocular_depth_estimation_trt_amd import flops
         lf = flops.layer_flops(cfg, size, size, B)
+    for name in layer_ms:
+        if name.endswith(".mlp") and name not in lf:   # fused fc1 + GELU + fc2 (csrc/mlp_fused.hip)
+            base = name[:-len(".mlp")]
+            lf[name] = lf.get(base + ".fc1", 0.0) + lf.get(base + ".fc2", 0.0)
     cls_ms, cls_fl, cls_n = {}, {}, {}
     for name, ms in layer_ms.items():
         c = flops.layer_class(name)
@@ -137,7 +150,7 @@ def roofline(cfg, B, size, layer_ms):
     breakdown = {c: {"ms": round(cls_ms[c], 4), "launches": cls_n[c],
                      "tflops": round(cls_fl[c] / (cls_ms[c] * 1e-3) / 1e12, 1) if cls_fl.get(c) else None}
                  for c in sorted(cls_ms, key=lambda c: -cls_ms[c])}
-    traffic, src = pmc_traffic(dom, cfg, B, size) if cfg.get("family") != "depth_pro" else (None, None)
+    traffic, src = pmc_traffic(dom, cfg, B, size) if fam not in ("depth_pro", "vggt") else (None, None)
     roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
             "flop_per_launch": per_launch_fl, "avg_launch_ms": round(avg_ms, 5),
@@ -210,6 +223,14 @@ def cpu_baseline(cfg, size, seconds):
         x = torch.from_numpy(WD.synthetic_images(1, size, first_seed=0))
         n, el = _timed_cpu(lambda: depth_pro_ref.forward(w, cfg, x), seconds, warmup=False, max_n=1)
         what = f"{n} x Depth Pro {size}x{size} batch-1 fp32 forward of oracle/depth_pro_ref.py (torch CPU), no warmup"
+    elif cfg.get("family") == "vggt":
+        # ~3.3 TFLOP per frame: the sample is ONE single-frame forward, no warmup
+        from oracle import vggt_ref
+        from monocular_depth_estimation_trt_amd import weights_vggt as WV
+        w = vggt_ref.to_torch(WV.synthetic_state_dict(cfg, 2468))
+        x = torch.from_numpy(WV.synthetic_images(1, 1, size, first_seed=0))
+        n, el = _timed_cpu(lambda: vggt_ref.forward(w, cfg, x), seconds, warmup=False, max_n=1)
+        what = f"{n} x VGGT-1B depth path {size}x{size} S=1 fp32 forward of oracle/vggt_ref.py (torch CPU), no warmup"
     else:
         from oracle import dav2_ref
         from monocular_depth_estimation_trt_amd import weights
@@ -227,6 +248,8 @@ class Workload:
 
     def __init__(self, a, rank):
         import torch
+        self.frames = 1
+        self.input_name = "input"
         if a.model == "depth_pro":
             from monocular_depth_estimation_trt_amd import pack_depth_pro as PD
             from monocular_depth_estimation_trt_amd import weights_depth_pro as WD
@@ -245,6 +268,26 @@ class Workload:
                              f"batch {B} per GPU, inputs resident in HBM, hipGraph replay")
             self.weights = "synthetic seeded (seed 4321), fan-in scaled"
             self.encoder = "dinov2l16_384"
+        elif a.model == "vggt":
+            from monocular_depth_estimation_trt_amd import pack_vggt as PV
+            from monocular_depth_estimation_trt_amd import weights_vggt as WV
+            from monocular_depth_estimation_trt_amd.flops_vggt import total_flops
+            self.cfg = WV.vggt_config("vggt_1b")
+            self.S = S = self.cfg["img"]
+            self.B = B = a.batch or 8
+            self.frames = Fr = a.frames
+            self.input_name = "images"
+            self.sd = WV.synthetic_state_dict(self.cfg, 2468)
+            self.blob = PV.pack_bytes(self.sd, self.cfg, Fr)
+            self.images = lambda n, seed: WV.synthetic_images(n, Fr, S, first_seed=seed * Fr)  # noqa: E731
+            self.outs = {"depth": (B, Fr, S, S, 1)}
+            self.gflop = total_flops(self.cfg, 1, Fr) / Fr / 1e9          # per frame
+            self.ref_fps = REF_VGGT_B1_FPS
+            self.label = "VGGT-1B depth"
+            self.workload = (f"VGGT-1B depth path (DINOv2-L/14-reg + 24 frame/global block pairs + DPT) {S}x{S}, "
+                             f"S={Fr} frames, forward, batch {B} per GPU, inputs resident in HBM, hipGraph replay")
+            self.weights = "synthetic seeded (seed 2468), fan-in scaled"
+            self.encoder = "vggt_1b"
         else:
             from monocular_depth_estimation_trt_amd import pack, weights
             from monocular_depth_estimation_trt_amd.flops import total_flops
@@ -298,8 +341,8 @@ def main():
     shape = tuple(wl.x.shape)
     eng = Engine.from_bytes(wl.blob, local, profile=((1,) + shape[1:], shape, shape))
     ctx = eng.create_execution_context()
-    ctx.set_input_shape("input", shape)
-    ctx.set_tensor_address("input", wl.x.data_ptr())
+    ctx.set_input_shape(wl.input_name, shape)
+    ctx.set_tensor_address(wl.input_name, wl.x.data_ptr())
     for k, t in wl.y.items():
         ctx.set_tensor_address(k, t.data_ptr())
     st = torch.cuda.Stream()
@@ -313,7 +356,7 @@ def main():
                                dist.barrier if dist is not None else None)
     el = replicas.max_over_ranks(el)
     out_ok = all(bool(torch.isfinite(t).all().item()) for t in wl.y.values())
-    value = world * B * a.steps / el
+    value = world * B * wl.frames * a.steps / el
     ms_step = el / a.steps * 1e3
 
     if rank != 0:
@@ -323,10 +366,11 @@ def main():
         return
 
     layer_ms = profile_layers(ctx, sh, a.profile_iters)
-    roof, breakdown = roofline(wl.cfg, B, S, layer_ms)
+    roof, breakdown = roofline(wl.cfg, B, S, layer_ms, wl.frames)
     if a.layers_json:
         with open(a.layers_json, "w") as f:
-            json.dump({"batch": B, "layer_ms": layer_ms, "classes": breakdown, "roofline": roof}, f, indent=1)
+            json.dump({"batch": B, "frames": wl.frames, "layer_ms": layer_ms, "classes": breakdown, "roofline": roof},
+                      f, indent=1)
     model_frac = value / world * wl.gflop * 1e9 / (MFMA_PEAK_TFLOPS * 1e12)
     ctx.destroy()
     eng.destroy()
@@ -336,14 +380,17 @@ def main():
         cpu = cpu_baseline(wl.cfg, S, a.cpu_seconds)
     for c, v in list(breakdown.items())[:10]:
         log(f"{c:24s} {v['ms']:9.4f} ms  x{v['launches']:3d}  {v['tflops']} TF/s")
+    config = {"workload": wl.workload, "encoder": wl.encoder, "img": [S, S], "batch_per_gpu": B,
+              "global_batch": B * world, "parallelism": f"replica x{world} (batch shards, no collectives)",
+              "weights": wl.weights}
+    if a.model == "vggt":
+        config["frames"] = wl.frames
     line = {
         "metric": f"depth FPS (images/s) at {S}x{S} fp16, {wl.label}, MI355X",
         "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
         "vs_baseline": round(value / wl.ref_fps, 3), "dtype": "fp16", "data": "synthetic",
-        "config": {"workload": wl.workload, "encoder": wl.encoder, "img": [S, S], "batch_per_gpu": B,
-                   "global_batch": B * world, "parallelism": f"replica x{world} (batch shards, no collectives)",
-                   "weights": wl.weights},
+        "config": config,
         "model_gflop_per_image": round(wl.gflop, 2),
         "model_mfma_frac": round(model_frac, 4),
         "roofline": roof,

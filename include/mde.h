@@ -15,6 +15,8 @@
  *                 get_tensor_name/shape/dtype/mode, get_tensor_profile_shape)
  *                 Depth Pro: models/depth_pro/onnx2trt.py:94-111 (same engine API,
  *                 outputs "canonical_inverse_depth" + "fov_deg", onnx_export.py:56)
+ *                 VGGT: models/vggt/onnx2trt.py:95-107 (input "images" [1,S,3,518,518],
+ *                 output "depth", onnx_export.py:125-127)
  *   context       engine.create_execution_context()
  *                 (models/depth_anything_v2/onnx2trt.py:93-94),
  *                 context.set_tensor_address (core/common_runtime.py:272-274),
@@ -40,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MDE_ABI_VERSION 3
+#define MDE_ABI_VERSION 4
 
 typedef enum {
   MDE_OK = 0,
@@ -78,7 +80,9 @@ typedef struct {
   int32_t input_format; /* 0: "input" float32 NCHW [B,3,H,W]; 1: "image_u8" uint8 NHWC [B,H,W,3] */
   int32_t family;       /* 0: Depth Anything V2 (io "input" -> "output" [B,H,W]);
                            1: Depth Pro (io "input" [B,3,1536,1536] -> "canonical_inverse_depth"
-                              [B,1,1536,1536] and, with the FOV head, "fov_deg" [B]) */
+                              [B,1,1536,1536] and, with the FOV head, "fov_deg" [B]);
+                           2: VGGT depth path (io "images" float32 [B,S,3,H,W] in [0,1] ->
+                              "depth" [B,S,H,W,1]; S fixed at pack time) */
 } mde_engine_info;
 
 /* IProfiler.report_layer_time analogue: one call per launched layer. */
@@ -190,6 +194,30 @@ int mde_op_dp_pyramid_patches(const float* img, int batch, int size, void* patch
  * gamma/beta non-null: LayerNorm(eps) fused into the gather, else a plain fp32 -> f16 copy. */
 int mde_op_merge_tokens(const float* x32, int batch, int tokens, int dim, int n, int g, int pad, int base,
                         const float* gamma, const float* beta, float eps, void* out_f16, void* stream);
+/* VGGT attention prologue (upstream vggt layers/attention.py q_norm / k_norm + layers/rope.py
+ * RotaryPositionEmbedding2D, base 100), in place on the head-major rows q/k [bh][tokens_pad][64]
+ * f16 (the layout mde_op_qkv writes): LayerNorm(64, eps) with q_gamma/q_beta resp. k_gamma/k_beta,
+ * then 2D RoPE -- token t sits at frame position p = t % frame_tokens; p < npre is at RoPE
+ * position (0, 0), patch p - npre at (row + 1, col + 1) of a grid grid_w wide; features [0, 32)
+ * rotate with the row, [32, 64) with the column (rotate_half inside each half); rope_cos /
+ * rope_sin are fp32 [>= max position + 1][16] tables of angle(pos, j) = pos * 100^(-j/16) --
+ * and finally q *= q_scale.  Rows >= tokens are not touched. */
+int mde_op_qk_norm_rope(void* q_f16, void* k_f16, const float* q_gamma, const float* q_beta, const float* k_gamma,
+                        const float* k_beta, int bh, int tokens, int tokens_pad, int frame_tokens, int npre,
+                        int grid_w, const float* rope_cos, const float* rope_sin, float q_scale, float eps,
+                        void* stream);
+/* VGGT depth-head tap (upstream heads/dpt_head.py: self.norm over aggregated_tokens_list[i]
+ * [:, :, patch_start_idx:], the list entries being cat(frame_out, global_out)): LayerNorm(2*dim,
+ * eps) over cat(xa[row], xb[row]) for the patch rows npre .. tokens-1 of each of nseq sequences
+ * (xa, xb fp32 [nseq][tokens][dim]) -> f16 [nseq * (tokens - npre)][2*dim]. */
+int mde_op_tap_concat_ln(const float* xa, const float* xb, int nseq, int tokens, int npre, int dim,
+                         const float* gamma, const float* beta, float eps, void* out_f16, void* stream);
+/* Fused ViT-S MLP + LayerScale residual (upstream DINOv2 Block ffn):
+ * x32[m] += ls2 * (GELU(a[m] . w1^T + b1) . w2^T + b2), the hidden activation rounded to f16 as
+ * the unfused fc1 stores it; a f16 [m][dim], w1 [hidden][ldw1], w2 [dim][ldw2]; supported:
+ * dim 384, hidden 1536, ldw1 384, ldw2 1536 (else MDE_ERR_ARG). */
+int mde_op_mlp_residual(const void* a_f16, int m, const void* w1_f16, int ldw1, const float* b1, const void* w2_f16,
+                        int ldw2, const float* b2, const float* ls2, float* x32, int dim, int hidden, void* stream);
 
 #ifdef __cplusplus
 }

@@ -21,7 +21,7 @@ LIB = os.path.join(HERE, "libmde_hip.so")
 OBJDIR = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("MDE_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["gemm.hip", "gemm_persistent.hip", "conv.hip", "attention.hip", "elementwise.hip", "engine.hip",
-           "depth_pro.hip", "depth_pro_ops.hip", "gemm256.hip"]
+           "depth_pro.hip", "depth_pro_ops.hip", "gemm256.hip", "vggt.hip", "vggt_ops.hip", "mlp_fused.hip"]
 # attention: no NaN inputs by construction (masked keys are -inf, never NaN);
 # lets fmaxf lower to a bare v_max_f32 without canonicalising moves
 PER_FILE = {"attention.hip": ["-fno-honor-nans"]}

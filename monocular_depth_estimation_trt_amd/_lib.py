@@ -107,6 +107,11 @@ PROTOTYPES = {
                             c_void_p, c_void_p],
     "mde_op_depth_postprocess": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_int, c_float, c_float,
                                  c_void_p],
+    "mde_op_qk_norm_rope": [c_void_p] * 6 + [c_int] * 6 + [c_void_p, c_void_p, c_float, c_float, c_void_p],
+    "mde_op_tap_concat_ln": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p,
+                             c_void_p],
+    "mde_op_mlp_residual": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
+                            c_void_p, c_int, c_int, c_void_p],
 }
 _RESTYPE = {"mde_last_error": c_char_p}
 

@@ -12,6 +12,7 @@ source, RuntimeError for a failed build/load).
 Source strings:
   synthetic:<vits|vitb|vitl>[:<metric|relative>[:<seed>]]   seeded DA-V2 weights
   synthetic:depth_pro[:<dinov2l16_384|tiny>[:<seed>]]       seeded Depth Pro weights
+  synthetic:vggt[:<vggt_1b|vggt_1b_shallow|tiny>[:<seed>]]  seeded VGGT weights (depth path)
   /path/ckpt.pth          torch.load(..., weights_only=True)
   /path/ckpt.safetensors  safetensors
   /path/ckpt.npz          numpy (allow_pickle=False)
@@ -26,7 +27,7 @@ from typing import Optional, Sequence
 
 import numpy as np
 
-from . import pack, pack_depth_pro, weights, weights_depth_pro
+from . import pack, pack_depth_pro, pack_vggt, weights, weights_depth_pro, weights_vggt
 from .common_runtime import *  # noqa: F401,F403  (re-export, as core/common.py does)
 from .engine import Engine
 
@@ -79,6 +80,26 @@ def is_depth_pro_source(src: str, sd: Optional[dict] = None) -> bool:
     return sd is not None and any(k.startswith("depth_pro.encoder.") for k in sd)
 
 
+def is_vggt_source(src: str, sd: Optional[dict] = None) -> bool:
+    """VGGT sources: synthetic:vggt[...] or an upstream-keyed VGGT state dict
+    (facebook/VGGT-1B model.pt: aggregator.frame_blocks.*)."""
+    if src.startswith("synthetic:"):
+        return src.split(":")[1] == "vggt"
+    return sd is not None and any(k.startswith("aggregator.frame_blocks.") for k in sd)
+
+
+def _vggt_config_of(sd: dict) -> dict:
+    """The VGGT preset a checkpoint matches (embed dim and block counts)."""
+    D = np.asarray(sd["aggregator.camera_token"]).shape[-1]
+    nfb = len({k.split(".")[2] for k in sd if k.startswith("aggregator.frame_blocks.")})
+    ndb = len({k.split(".")[3] for k in sd if k.startswith("aggregator.patch_embed.blocks.")})
+    for preset in weights_vggt.PRESETS:
+        cfg = weights_vggt.vggt_config(preset)
+        if cfg["embed_dim"] == D and cfg["aa_depth"] == nfb and cfg["depth"] == ndb:
+            return cfg
+    raise ValueError(f"no VGGT preset matches this checkpoint (dim {D}, {ndb} + {nfb} blocks)")
+
+
 def _depth_pro_config_of(sd: dict) -> dict:
     """The Depth Pro preset a checkpoint matches (by ViT width / depth and the FOV head)."""
     D = np.asarray(sd["depth_pro.encoder.patch_encoder.model.embeddings.cls_token"]).shape[-1]
@@ -102,12 +123,14 @@ def _infer_encoder(sd: dict) -> str:
 
 def _engine_fingerprint(src, precision, workspace_gib, opt_level, obey_precision_constraints,
                         dynamic_input_shapes, encoder, depth_type, max_depth, input_hw,
-                        input_format="float32_nchw") -> str:
+                        input_format="float32_nchw", frames=None) -> str:
     parts = [_source_digest(src), f"packer={pack.PACKER_VERSION}", f"precision={precision}",
              f"workspace={workspace_gib}", f"opt_level={opt_level}",
              f"obey_precision={obey_precision_constraints}", f"dynamic={dynamic_input_shapes}",
              f"encoder={encoder}", f"depth_type={depth_type}", f"max_depth={max_depth}",
              f"input_hw={tuple(input_hw)}", f"input_format={input_format}", "arch=gfx950"]
+    if frames is not None:
+        parts.append(f"frames={frames}")
     return "\n".join(parts)
 
 
@@ -132,13 +155,16 @@ def get_engine(onnx_file_path, engine_file_path="", precision="fp32", dynamic_in
                workspace_gib=2, opt_level=None, obey_precision_constraints=False, check_fingerprint=True,
                *, encoder: Optional[str] = None, depth_type: Optional[str] = None,
                max_depth: Optional[float] = None, input_hw: Optional[Sequence[int]] = None,
-               input_format: str = "float32_nchw", device: int = 0) -> Engine:
+               input_format: str = "float32_nchw", device: int = 0, frames: Optional[int] = None) -> Engine:
     """Load `engine_file_path` if it matches its source, otherwise pack it.
 
     `onnx_file_path` keeps the reference's parameter name; it names the
     checkpoint / synthetic spec the engine is packed from.
     `dynamic_input_shapes` = [min, opt, max] input shapes gives a
-    dynamic-batch engine whose contexts are sized for max[0].
+    dynamic-batch engine whose contexts are sized for max[0] (VGGT: rank-5
+    [B, S, 3, H, W] shapes, S fixed).
+    `frames` (VGGT): the frame count S the engine is packed for (default 1,
+    or the S of the dynamic shapes).
     `precision`: "fp16" (the engine's arithmetic: f16 operands, fp32
     accumulation/statistics).  "fp32" raises -- there is no fp32 engine.
     `input_format` "uint8_nhwc" packs the reference's uint8 preamble
@@ -160,7 +186,11 @@ def get_engine(onnx_file_path, engine_file_path="", precision="fp32", dynamic_in
             raise ValueError("[MDET] only the batch dimension may be dynamic")
         if not (1 <= mn[0] <= opt[0] <= mx[0]):
             raise ValueError(f"[MDET] bad batch profile {mn[0]}/{opt[0]}/{mx[0]}")
-        input_hw = input_hw or ((mn[1], mn[2]) if u8 else (mn[2], mn[3]))
+        if len(mn) == 5:       # VGGT [B, S, 3, H, W]
+            input_hw = input_hw or (mn[3], mn[4])
+            frames = frames or mn[1]
+        else:
+            input_hw = input_hw or ((mn[1], mn[2]) if u8 else (mn[2], mn[3]))
         profile = (mn, opt, mx)
     else:
         profile = None
@@ -182,7 +212,15 @@ def get_engine(onnx_file_path, engine_file_path="", precision="fp32", dynamic_in
     if check_fingerprint and present and engine_file_path:
         fingerprint = _engine_fingerprint(src, precision, workspace_gib, opt_level, obey_precision_constraints,
                                           dynamic_input_shapes, encoder, depth_type, max_depth, input_hw,
-                                          input_format)
+                                          input_format, frames)
+
+    def build_vggt(sd_, cfg) -> bytes:
+        if u8:
+            raise ValueError("[MDET] VGGT engines take float32 [B, S, 3, H, W] images (no uint8 preamble)")
+        if tuple(input_hw) != (cfg["img"], cfg["img"]):
+            raise ValueError(f"[MDET] VGGT packs at its checkpoint grid {cfg['img']}x{cfg['img']}, "
+                             f"not {tuple(input_hw)}")
+        return pack_vggt.pack_bytes(sd_, cfg, int(frames or 1))
 
     def build_engine() -> bytes:
         nonlocal sd, encoder
@@ -193,10 +231,17 @@ def get_engine(onnx_file_path, engine_file_path="", precision="fp32", dynamic_in
             cfg = weights_depth_pro.depth_pro_config(parts[2] if len(parts) > 2 and parts[2] else "dinov2l16_384")
             sd = weights_depth_pro.synthetic_state_dict(cfg, int(parts[3]) if len(parts) > 3 and parts[3] else 4321)
             return pack_depth_pro.pack_bytes(sd, cfg)
+        if is_vggt_source(src):
+            parts = src.split(":")
+            cfg = weights_vggt.vggt_config(parts[2] if len(parts) > 2 and parts[2] else "vggt_1b")
+            sd = weights_vggt.synthetic_state_dict(cfg, int(parts[3]) if len(parts) > 3 and parts[3] else 2468)
+            return build_vggt(sd, cfg)
         if not src.startswith("synthetic:"):
             sd = load_checkpoint(src)
             if is_depth_pro_source(src, sd):
                 return pack_depth_pro.pack_bytes(sd, _depth_pro_config_of(sd))
+            if is_vggt_source(src, sd):
+                return build_vggt(sd, _vggt_config_of(sd))
         if src.startswith("synthetic:"):
             cfg = weights.model_config(encoder, depth_type, max_depth)
             sd = weights.synthetic_state_dict(cfg, _parse_synthetic(src)[2])

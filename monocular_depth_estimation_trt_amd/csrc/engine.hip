@@ -1,6 +1,7 @@
 // libmde_hip engine: packed-weight loader, execution context and the DA-V2
 // forward schedule, behind the C ABI of include/mde.h.  The Depth Pro
-// schedule lives in depth_pro.hip; both share engine_internal.h.
+// schedule lives in depth_pro.hip, VGGT's in vggt.hip; all share
+// engine_internal.h.
 //
 // Replaces TensorRT's ICudaEngine / IExecutionContext as used by the
 // reference (core/common.py:141-312, core/common_runtime.py:131-275): one
@@ -101,7 +102,7 @@ int load_pack(const uint8_t* data, size_t n, int device, mde_engine** out) {
   e->device = device;
   memcpy(&e->cfg, data + sizeof(PackHeader), sizeof(PackConfig));
   e->family = e->cfg.family;
-  if (e->family != FAMILY_DAV2 && e->family != FAMILY_DEPTH_PRO) {
+  if (e->family != FAMILY_DAV2 && e->family != FAMILY_DEPTH_PRO && e->family != FAMILY_VGGT) {
     delete e;
     return fail(MDE_ERR_FORMAT, "unknown model family in packed config");
   }
@@ -120,7 +121,9 @@ int load_pack(const uint8_t* data, size_t n, int device, mde_engine** out) {
     pt.name[sizeof(pt.name) - 1] = 0;
     e->t[pt.name] = dt;
   }
-  const std::string bad = e->family == FAMILY_DAV2 ? setup_dav2(e) : setup_depth_pro(e);
+  const std::string bad = e->family == FAMILY_DAV2        ? setup_dav2(e)
+                          : e->family == FAMILY_DEPTH_PRO ? setup_depth_pro(e)
+                                                          : setup_vggt(e);
   if (!bad.empty()) {
     delete e;
     return fail(MDE_ERR_FORMAT, bad);
@@ -195,6 +198,7 @@ namespace {
 
 size_t plan_arena(const mde_engine& e, int B, mde_context* c, uint8_t* base) {
   if (e.family == FAMILY_DEPTH_PRO) return plan_arena_dp(e, B, c ? &c->d : nullptr, base);
+  if (e.family == FAMILY_VGGT) return plan_arena_vggt(e, B, c ? &c->v : nullptr, base);
   return plan_arena_dav2(e, B, c ? &c->b : nullptr, base);
 }
 
@@ -265,6 +269,9 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
   int tap = 0;
   char nm[64];
   const bool fuse = fuse_ln_enabled() && (D == 384 || D == 768 || D == 1024);
+  // fc1 + GELU + fc2 + LayerScale residual in one kernel (ViT-S; mlp_fused.hip)
+  const bool fused_mlp = !fuse && mlp_fused_supported(D, cf.mlp_hidden, ldw("b0.fc1.w"), ldw("b0.fc2.w")) &&
+                         mlp_fused_enabled(B * T);
   // fused LayerNorm in a residual GEMM's tail: out1 = LN(g1,b1) (token
   // layout), out2 = final norm into a tap map (cls dropped)
   auto fuse_ln = [&](GemmParams& g, const char* g1, const char* b1, h16* tapdst) {
@@ -327,7 +334,20 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
         return launch_layernorm(b.X, b.Hn, w32(p + "ln2.g"), w32(p + "ln2.b"), B * T, D, cf.ln_eps, T, 0, st);
       });
     }
-    {
+    if (fused_mlp) {
+      MlpParams mp;
+      mp.A = b.Hn;
+      mp.M = B * T;
+      mp.W1 = w16(p + "fc1.w");
+      mp.b1 = w32(p + "fc1.b");
+      mp.W2 = w16(p + "fc2.w");
+      mp.ldw2 = ldw(p + "fc2.w");
+      mp.b2 = w32(p + "fc2.b");
+      mp.ls2 = w32(p + "ls2");
+      mp.x32 = b.X;
+      snprintf(nm, sizeof nm, "block%d.mlp", i);
+      step(nm, [&] { return launch_mlp_fused(mp, st); });
+    } else {
       GemmParams g = dense(b.Hn, D, p + "fc1.w", B * T, cf.mlp_hidden, D);
       g.emode = E_STORE;
       g.bias = w32(p + "fc1.b");
@@ -337,7 +357,7 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
       snprintf(nm, sizeof nm, "block%d.fc1", i);
       gemm(nm, g);
     }
-    {
+    if (!fused_mlp) {
       GemmParams g = dense(b.Mh, cf.mlp_hidden, p + "fc2.w", B * T, D, cf.mlp_hidden);
       g.emode = E_RESID;
       g.bias = w32(p + "fc2.b");
@@ -484,7 +504,9 @@ int check_ctx(const mde_context* c) {
   return MDE_OK;
 }
 
-const char* input_name(const mde_engine* e) { return e->cfg.input_u8 ? "image_u8" : "input"; }
+const char* input_name(const mde_engine* e) {
+  return e->family == FAMILY_VGGT ? "images" : e->cfg.input_u8 ? "image_u8" : "input";
+}
 bool is_input(const mde_engine* e, const char* n) { return n && strcmp(n, input_name(e)) == 0; }
 
 // io binding index of a tensor name (0 = input, 1 = depth output, 2 = fov), -1 if unknown
@@ -501,6 +523,7 @@ int io_index(const mde_engine* e, const char* n) {
 
 hipError_t run_forward(Runner& r, int B, const void* in, float* out, float* out2) {
   if (r.c.e->family == FAMILY_DEPTH_PRO) return r.forward_dp(B, (const float*)in, out, out2);
+  if (r.c.e->family == FAMILY_VGGT) return r.forward_vggt(B, (const float*)in, out);
   return r.forward_dav2(B, in, out);
 }
 
@@ -595,6 +618,28 @@ int mde_engine_num_io(const mde_engine* e, int* n) {
 int mde_engine_io_desc(const mde_engine* e, int index, mde_io_desc* o) {
   if (!e || !o) return fail(MDE_ERR_ARG, "null argument");
   memset(o, 0, sizeof *o);
+  if (e->family == FAMILY_VGGT) {
+    // reference input_names=["images"] [1,S,3,518,518], output_names=["depth"]
+    // (models/vggt/onnx_export.py:101,125-127); S fixed at pack time
+    if (index < 0 || index > 1) return fail(MDE_ERR_ARG, "io index out of range");
+    o->dtype = MDE_FLOAT32;
+    o->is_input = index == 0;
+    o->rank = 5;
+    o->dims[0] = -1;
+    o->dims[1] = e->S;
+    if (index == 0) {
+      strcpy(o->name, "images");
+      o->dims[2] = 3;
+      o->dims[3] = e->cfg.img_h;
+      o->dims[4] = e->cfg.img_w;
+    } else {
+      strcpy(o->name, "depth");
+      o->dims[2] = e->cfg.img_h;
+      o->dims[3] = e->cfg.img_w;
+      o->dims[4] = 1;
+    }
+    return MDE_OK;
+  }
   if (index == 0 && e->cfg.input_u8) {
     strcpy(o->name, "image_u8");
     o->dtype = MDE_UINT8;
@@ -718,7 +763,13 @@ int mde_context_set_input_shape(mde_context* c, const char* name, const int64_t*
   if (int rc = check_ctx(c)) return rc;
   if (!is_input(c->e, name)) return fail(MDE_ERR_NAME, std::string("not an input: ") + (name ? name : "(null)"));
   const PackConfig& cf = c->e->cfg;
-  if (cf.input_u8) {
+  if (c->e->family == FAMILY_VGGT) {
+    const int S = c->e->S;
+    if (!dims || rank != 5) return fail(MDE_ERR_SHAPE, "input shape must be rank 5 [B,S,3,H,W]");
+    if (dims[1] != S || dims[2] != 3 || dims[3] != cf.img_h || dims[4] != cf.img_w)
+      return fail(MDE_ERR_SHAPE, "input shape must be [B," + std::to_string(S) + ",3," + std::to_string(cf.img_h) +
+                                     "," + std::to_string(cf.img_w) + "] for this engine");
+  } else if (cf.input_u8) {
     if (!dims || rank != 4) return fail(MDE_ERR_SHAPE, "input shape must be rank 4 [B,H,W,3]");
     if (dims[3] != 3 || dims[1] != cf.img_h || dims[2] != cf.img_w)
       return fail(MDE_ERR_SHAPE, "input shape must be [B," + std::to_string(cf.img_h) + "," +
@@ -969,6 +1020,47 @@ int mde_op_merge_tokens(const float* x32, int batch, int tokens, int dim, int n,
   m.base = base;
   m.T = tokens;
   OP_RET(launch_merge_tokens(x32, (h16*)out, gamma, beta, dim, m, eps, (hipStream_t)st), "merge_tokens");
+}
+
+int mde_op_qk_norm_rope(void* q, void* k, const float* qg, const float* qb, const float* kg, const float* kb, int bh,
+                        int tokens, int tokens_pad, int frame_tokens, int npre, int grid_w, const float* rope_cos,
+                        const float* rope_sin, float q_scale, float eps, void* st) {
+  if (!q || !k || !qg || !qb || !kg || !kb || !rope_cos || !rope_sin) return fail(MDE_ERR_ARG, "null argument");
+  RopeGeom geo;
+  geo.T = tokens;
+  geo.Tpad = tokens_pad;
+  geo.P = frame_tokens;
+  geo.npre = npre;
+  geo.gw = grid_w;
+  geo.qscale = q_scale;
+  geo.eps = eps;
+  OP_RET(launch_qk_norm_rope((h16*)q, (h16*)k, qg, qb, kg, kb, rope_cos, rope_sin, bh, geo, (hipStream_t)st),
+         "qk_norm_rope");
+}
+
+int mde_op_tap_concat_ln(const float* xa, const float* xb, int nseq, int tokens, int npre, int dim, const float* g,
+                         const float* b, float eps, void* out, void* st) {
+  if (!xa || !xb || !g || !b || !out || nseq < 0) return fail(MDE_ERR_ARG, "null argument");
+  OP_RET(launch_tap_concat_ln(xa, xb, (h16*)out, g, b, nseq, tokens, npre, dim, eps, (hipStream_t)st),
+         "tap_concat_ln");
+}
+
+int mde_op_mlp_residual(const void* a, int m, const void* w1, int ldw1, const float* b1, const void* w2, int ldw2,
+                        const float* b2, const float* ls2, float* x32, int dim, int hidden, void* st) {
+  if (!a || !w1 || !b1 || !w2 || !b2 || !ls2 || !x32) return fail(MDE_ERR_ARG, "null argument");
+  if (!mlp_fused_supported(dim, hidden, ldw1, ldw2))
+    return fail(MDE_ERR_ARG, "mde_op_mlp_residual: only dim 384 / hidden 1536 (ViT-S) with dense weights");
+  MlpParams mp;
+  mp.A = (const h16*)a;
+  mp.M = m;
+  mp.W1 = (const h16*)w1;
+  mp.b1 = b1;
+  mp.W2 = (const h16*)w2;
+  mp.ldw2 = ldw2;
+  mp.b2 = b2;
+  mp.ls2 = ls2;
+  mp.x32 = x32;
+  OP_RET(launch_mlp_fused(mp, (hipStream_t)st), "mlp_residual");
 }
 
 int mde_op_layernorm(const float* x, void* y, const float* g, const float* b, int rows, int dim, float eps,

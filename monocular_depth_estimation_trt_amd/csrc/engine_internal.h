@@ -55,7 +55,19 @@ struct DPBuf {
   h16 *fv1, *fv2, *fv3;            // fov head
 };
 
-enum Family : int { FAMILY_DAV2 = 0, FAMILY_DEPTH_PRO = 1 };
+// VGGT activations (vggt.hip plan_arena_vggt) over n = B*S frames.
+struct VGBuf {
+  h16* P;                  // patch-embed rows [n*np][672]
+  float *X, *Xf;           // residual stream [n][T][D]; frame-block output snapshot at the taps
+  h16 *Hn, *O, *Mh;        // block scratch
+  h16 *Q, *K, *Vt;         // frame attention operands [n*H][Tpad][64]
+  h16 *Qg, *Kg, *Vg;       // global attention operands [B*H][Tgpad][64] (alias Q/K/Vt when S == 1)
+  h16* tap;                // LN(cat(frame, global)) patch tokens [n*np][2D]
+  h16 *pj[4], *l1, *l2, *l4, *rn[4];
+  h16 *tb, *sb, *ub, *vb, *p4, *p3, *p2, *c1;
+};
+
+enum Family : int { FAMILY_DAV2 = 0, FAMILY_DEPTH_PRO = 1, FAMILY_VGGT = 2 };
 
 }  // namespace mde
 
@@ -76,6 +88,9 @@ struct mde_engine {
   int lev_n[3] = {0, 0, 0}, lev_pad[3] = {0, 0, 0}, lev_base[3] = {0, 0, 0}, lev_stride[3] = {0, 0, 0};
   int lev_f[3] = {0, 0, 0};  // downsample factor of the level (4, 2, 1)
   float fov_b = 0.f;
+  // VGGT geometry: npre special tokens per frame, S frames per batch item,
+  // Tg = S * T tokens per global-attention sequence (padded to Tgpad)
+  int npre = 0, S = 1, Tg = 0, Tgpad = 0;
 
   const mde::DevTensor* get(const std::string& n) const {
     auto it = t.find(n);
@@ -109,6 +124,7 @@ struct mde_context {
   size_t arena_bytes = 0;
   mde::DAV2Buf b{};
   mde::DPBuf d{};
+  mde::VGBuf v{};
   bool graph_mode = true;
   hipStream_t cap_stream = nullptr;
   std::map<mde::GraphKey, std::pair<hipGraph_t, hipGraphExec_t>> graphs;
@@ -136,9 +152,11 @@ struct ArenaPlan {
 
 size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base);
 size_t plan_arena_dp(const mde_engine& e, int B, DPBuf* b, uint8_t* base);
-// Depth Pro load-time checks (tensor presence, supported geometry); fills
-// the derived geometry.  Returns an error message or "".
+size_t plan_arena_vggt(const mde_engine& e, int B, VGBuf* b, uint8_t* base);
+// Load-time checks (tensor presence, supported geometry); fill the derived
+// geometry.  Return an error message or "".
 std::string setup_depth_pro(mde_engine* e);
+std::string setup_vggt(mde_engine* e);
 
 // The forward schedule: one method per model family, common helpers here.
 struct Runner {
@@ -233,7 +251,10 @@ struct Runner {
 
   // pre-activation residual conv unit:
   // out = conv2(relu(conv1(relu(x)) + b1)) + b2 + x (+ extra)
-  void rcu(const std::string& pfx, const h16* x, const h16* extra, h16* out, h16* tmp, int B, int h, int w, int F) {
+  // relu_res: the skip adds relu(x) instead of x (an nn.ReLU(inplace=True)
+  // activation overwrites the unit's input, as in VGGT's DPT head)
+  void rcu(const std::string& pfx, const h16* x, const h16* extra, h16* out, h16* tmp, int B, int h, int w, int F,
+           bool relu_res = false) {
     GemmParams g1 = conv(x, B, h, w, F, pfx + ".c1.w", F, 1);
     g1.relu_in = 1;
     g1.bias = w32_opt(pfx + ".c1.b");
@@ -243,6 +264,7 @@ struct Runner {
     GemmParams g2 = conv(tmp, B, h, w, F, pfx + ".c2.w", F, 1);
     g2.bias = w32_opt(pfx + ".c2.b");
     g2.res0 = x;
+    g2.res0_relu = relu_res ? 1 : 0;
     g2.res1 = extra;
     g2.out16 = out;
     gemm((pfx + ".c2").c_str(), g2);
@@ -252,6 +274,9 @@ struct Runner {
   void dav2_fusion(int r, const h16* x0, const h16* x1, int B, int h, int w, h16* dst, int oh, int ow);
   hipError_t forward_dp(int B, const float* img, float* out, float* fov);
   void dp_encoder(const std::string& pfx, float* X, const h16* P, int nseq, int hook_seqs);
+  hipError_t forward_vggt(int B, const float* img, float* out);
+  void vggt_block(const std::string& p, float eps, bool qk, int seqs, int T, int Tpad, h16* Q, h16* K, h16* Vt);
+  void vggt_fusion(int r, const h16* x0, const h16* x1, int n, int h, int w, h16* dst, int oh, int ow);
 };
 
 }  // namespace mde

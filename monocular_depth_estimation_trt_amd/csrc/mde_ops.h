@@ -19,9 +19,9 @@ enum EMode : int {
   E_STORE = 0,   // out16[m*ldo+n] = act(acc + bias[n]) (+ res0 + res1)
   E_QKV = 1,     // scatter to head-major q (pre-scaled), k and transposed v
   E_RESID = 2,   // x32[m*ldo+n] += ls[n] * (acc + bias[n])
-  E_PATCH = 3,   // x32[(b*T+1+p)*ldo+n] = acc + bias[n] + pos[p*ldo+n]
+  E_PATCH = 3,   // x32[(b*T+tok0+p)*ldo+n] = acc + bias[n] + pos[p*ldo+n]
   E_CONVT = 4,   // ConvTranspose(k=s) pixel-shuffle store into NHWC f16
-  E_HEAD = 5     // relu(acc+bias) . w2 + b2 -> sigmoid*max | relu -> fp32 map
+  E_HEAD = 5     // relu(acc+bias(+pe)) . w2 + b2 -> sigmoid*max | relu | exp -> fp32 map
 };
 
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
@@ -40,17 +40,24 @@ struct GemmParams {
   const float* bias = nullptr; int act = ACT_NONE;
   h16* out16 = nullptr; int ldo = 0;
   const h16* res0 = nullptr; const h16* res1 = nullptr;
+  // E_STORE residual options: res0_relu -> add relu(res0) (VGGT's in-place
+  // ReLU residual units); res0_rows > 0 -> res0 is a table of res0_rows rows
+  // repeated over m (row m % res0_rows: a per-image positional embedding)
+  int res0_relu = 0; int res0_rows = 0;
   float* x32 = nullptr; const float* ls = nullptr;
   // E_QKV
   h16 *q = nullptr, *k = nullptr, *vt = nullptr;
   int T = 0, Tpad = 0, heads = 0; float qscale = 1.0f;
-  // E_PATCH
-  const float* pos = nullptr; int npatch = 0;
+  // E_PATCH: patch rows start at token tok0 of each sequence (1 = after cls)
+  const float* pos = nullptr; int npatch = 0; int tok0 = 1;
   // E_CONVT
   int s = 0, cout = 0, ih = 0, iw = 0;
-  // E_HEAD
+  // E_HEAD: head_metric 0 ReLU, 1 max_depth * sigmoid, 2 exp; hpe (optional)
+  // = f16 [hpe_pix][32] added to the hidden layer before its ReLU at pixel
+  // m % hpe_pix (VGGT: the folded conv of the UV positional embedding)
   const float* w2 = nullptr; float b2 = 0.f; int head_metric = 1; float max_depth = 1.f;
   float* out32 = nullptr;
+  const h16* hpe = nullptr; int hpe_pix = 0;
   // E_RESID + fused LayerNorm of the finished rows (ln_counter != null): the
   // last workgroup of each row block normalises rows [m0, m0+BM) of x32 into
   // up to two f16 outputs (gamma/beta each; skip_cls -> tap token-map layout)
@@ -114,5 +121,37 @@ hipError_t launch_cls_rows(float* X, const float* cls, int nseq, int T, int D, h
 hipError_t launch_merge_tokens(const float* x, h16* y, const float* g, const float* b, int D, const DpMerge& m,
                                float eps, hipStream_t st);
 hipError_t launch_fov_final(const h16* in, const float* w, float bias, int K, int B, float* out, hipStream_t st);
+
+// ---- fused ViT-S MLP (mlp_fused.hip) ----
+struct MlpParams {
+  const h16* A = nullptr; int M = 0;                                  // LN output rows [M][384]
+  const h16* W1 = nullptr; const float* b1 = nullptr;                 // fc1 [1536][384]
+  const h16* W2 = nullptr; int ldw2 = 0; const float* b2 = nullptr;   // fc2 [384][ldw2]
+  const float* ls2 = nullptr; float* x32 = nullptr;                   // LayerScale, residual [M][384]
+};
+bool mlp_fused_supported(int dim, int hidden, int ldw1, int ldw2);
+bool mlp_fused_enabled(int M);  // MDE_FUSED_MLP: 0 off, 1 auto (>= 256 row blocks), 2 always
+hipError_t launch_mlp_fused(const MlpParams& p, hipStream_t st);
+
+// ---- VGGT (vggt_ops.hip) ----
+// Token geometry of the q/k rows one qk_norm_rope launch covers: T tokens per
+// sequence (rows padded to Tpad), P tokens per frame (T = S * P for global
+// attention), the first npre of each frame special (RoPE position (0, 0)),
+// the rest a grid gw wide at positions (row + 1, col + 1).
+struct RopeGeom {
+  int T = 0, Tpad = 0, P = 1, npre = 0, gw = 1;
+  float qscale = 1.f, eps = 1e-5f;
+};
+// special-token rows [0, npre) of every sequence from pre[sets][npre][D]
+// (sets 2: set 0 for the first frame of each batch item, 1 for the others)
+hipError_t launch_prefix_rows(float* X, const float* pre, int nseq, int T, int npre, int D, int frames, int sets,
+                              hipStream_t st);
+hipError_t launch_rows_layernorm(float* X, const float* g, const float* b, int nseq, int T, int row0, int D, float eps,
+                                 hipStream_t st);
+hipError_t launch_qk_norm_rope(h16* q, h16* k, const float* qg, const float* qb, const float* kg, const float* kb,
+                               const float* rope_cos, const float* rope_sin, int BH, const RopeGeom& geo,
+                               hipStream_t st);
+hipError_t launch_tap_concat_ln(const float* xa, const float* xb, h16* y, const float* g, const float* b, int nseq,
+                                int T, int npre, int D, float eps, hipStream_t st);
 
 }  // namespace mde

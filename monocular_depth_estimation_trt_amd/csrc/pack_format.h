@@ -34,14 +34,20 @@ struct PackConfig {
   // engine computes ((float)u / in_scale - in_mean[c]) / in_std[c] in fp32
   int32_t input_u8;
   float in_scale, in_mean[3], in_std[3];
-  // model family (0 = Depth Anything V2, 1 = Depth Pro) and the Depth Pro
-  // decoder geometry (HF DepthProConfig fields; zero for DA-V2).  For Depth
+  // model family (0 = Depth Anything V2, 1 = Depth Pro, 2 = VGGT) and the
+  // Depth Pro decoder geometry (HF DepthProConfig fields; zero otherwise).  For Depth
   // Pro, img_h/img_w = the fixed 1536 input, patch = 16, vit_size = 384,
   // features = fusion_hidden_size, metric = 0 (ReLU head).
   int32_t family;
   int32_t vit_size, merge_pad, use_fov, fov_layers, fov_k;
   int32_t hooks[2], inter_dims[2], scaled_dims[3];
-  char reserved[76];
+  // VGGT (family 2): embed_dim / depth / ln_eps above describe the DINOv2
+  // patch embedding, taps index the aggregator blocks, metric = 2 (exp head);
+  // frames = S (the packed frame count), npre = special tokens per frame (5),
+  // aa_depth = frame/global block pairs, agg_eps = aggregator / head LN eps
+  int32_t frames, npre, aa_depth;
+  float agg_eps;
+  char reserved[60];
 };
 static_assert(sizeof(PackConfig) == 256, "PackConfig");
 

@@ -11,27 +11,38 @@
 
 namespace mde {
 
+// E_STORE residual element offset of output element o = m*ldo + n: the row
+// of a repeated table (res0_rows > 0) or the output's own offset.
+MDE_DEV size_t res0_offset(const GemmParams& p, int m, int n, size_t o) {
+  return p.res0_rows > 0 ? (size_t)(m % p.res0_rows) * p.ldo + n : o;
+}
+
 template <int EM, int TM, int TN>
 MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&mrow)[TM], int ncol, int lane) {
   if constexpr (EM == E_HEAD) {
     static_assert(TN == 2, "head epilogue needs the full 32-channel row in one wave (BN 32, WN 1)");
 #pragma unroll
     for (int i = 0; i < TM; ++i) {
+      const int m = mrow[i];
+      const f16* pe = (p.hpe && m >= 0) ? reinterpret_cast<const f16*>(p.hpe) + (size_t)(m % p.hpe_pix) * 32 : nullptr;
       float part = 0.f;
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
+      for (int j = 0; j < TN; ++j) {
+        const int n0 = j * 16 + (lane >> 4) * 4;
+        f16x4 pv = {(f16)0.0f, (f16)0.0f, (f16)0.0f, (f16)0.0f};
+        if (pe) pv = *reinterpret_cast<const f16x4*>(pe + n0);
 #pragma unroll
         for (int r = 0; r < 4; ++r) {
-          const int n = j * 16 + (lane >> 4) * 4 + r;
-          const float v = acc[i][j][r] + p.bias[n];
-          part += (v > 0.f ? v : 0.f) * p.w2[n];
+          const float v = acc[i][j][r] + p.bias[n0 + r] + (float)pv[r];
+          part += (v > 0.f ? v : 0.f) * p.w2[n0 + r];
         }
+      }
       part += __shfl_xor(part, 16, 64);
       part += __shfl_xor(part, 32, 64);
-      const int m = mrow[i];
       if ((lane >> 4) == 0 && m >= 0) {
         const float z = part + p.b2;
-        p.out32[m] = p.head_metric ? p.max_depth / (1.f + __expf(-z)) : (z > 0.f ? z : 0.f);
+        p.out32[m] = p.head_metric == 2 ? __expf(z)
+                     : p.head_metric ? p.max_depth / (1.f + __expf(-z)) : (z > 0.f ? z : 0.f);
       }
     }
     return;
@@ -65,9 +76,15 @@ MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&m
           const size_t o = (size_t)m * p.ldo + n;
 #endif
           if (p.res0) {
-            const f16x4 r0 = *reinterpret_cast<const f16x4*>(reinterpret_cast<const f16*>(p.res0) + o);
+            const f16x4 r0 =
+                *reinterpret_cast<const f16x4*>(reinterpret_cast<const f16*>(p.res0) + res0_offset(p, m, n, o));
+            if (p.res0_relu) {
 #pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] += (float)r0[r];
+              for (int r = 0; r < 4; ++r) v[r] += fmaxf((float)r0[r], 0.f);
+            } else {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] += (float)r0[r];
+            }
           }
           if (p.res1) {
             const f16x4 r1 = *reinterpret_cast<const f16x4*>(reinterpret_cast<const f16*>(p.res1) + o);
@@ -108,7 +125,7 @@ MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&m
         } else if constexpr (EM == E_PATCH) {
           const int b = m / p.npatch, pi = m - (m / p.npatch) * p.npatch;
           const float4 ps = *reinterpret_cast<const float4*>(p.pos + (size_t)pi * p.ldo + n);
-          *reinterpret_cast<float4*>(p.x32 + ((size_t)b * p.T + 1 + pi) * p.ldo + n) =
+          *reinterpret_cast<float4*>(p.x32 + ((size_t)b * p.T + p.tok0 + pi) * p.ldo + n) =
               float4{v[0] + ps.x, v[1] + ps.y, v[2] + ps.z, v[3] + ps.w};
         } else if constexpr (EM == E_CONVT) {
           const int q = n / p.cout, co = n - q * p.cout;
@@ -201,9 +218,15 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
       if constexpr (EM == E_STORE) {
         const size_t o = (size_t)m * p.ldo + n;
         if (p.res0) {
-          const f16x8 r0 = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res0) + o);
+          const f16x8 r0 =
+              *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res0) + res0_offset(p, m, n, o));
+          if (p.res0_relu) {
 #pragma unroll
-          for (int r = 0; r < 8; ++r) v[r] += (float)r0[r];
+            for (int r = 0; r < 8; ++r) v[r] += fmaxf((float)r0[r], 0.f);
+          } else {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) v[r] += (float)r0[r];
+          }
         }
         if (p.res1) {
           const f16x8 r1 = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res1) + o);
