@@ -122,6 +122,37 @@ def pmc_traffic(cls, cfg, B, size):
     return None, None
 
 
+def pmc_traffic_vggt(cls, cfg, B, frames):
+    """VGGT: HBM bytes per launch of the dominant class's kernel from
+    profiles/traffic_vggt_b<B>_s<S>.json.  Token-major GEMMs are matched by
+    template + grid (work-items); proj and fc2 share the 128^2 E_RESID GEMM
+    and alternate in dispatch order (proj first in every block)."""
+    import re
+    path = os.path.join(ROOT, "profiles", f"traffic_vggt_b{B}_s{frames}.json")
+    if not os.path.exists(path):
+        return None, None
+    T = (cfg["img"] // cfg["patch"]) ** 2 + 5
+    M, D = B * frames * T, cfg["embed_dim"]
+    layer = cls.split(".")[-1]
+    if layer in ("proj", "fc2"):
+        pat, grid = r"gemm_kernel<128, 128, 64, 2, 2, 0, 2>", -(-M // 128) * -(-D // 128) * 256
+        phase = 0 if layer == "proj" else 1
+    elif layer == "attn":
+        seqs, L = (B, frames * T) if cls.startswith("gb") else (B * frames, T)
+        pat, grid, phase = r"attn_fwd_kernel", -(-L // 128) * seqs * cfg["num_heads"] * 512, None
+    else:
+        return None, None
+    with open(path) as f:
+        d = json.load(f)
+    for r in d["kernels"]:
+        if re.search(pat, r["kernel"]) and r["grid"] == grid:
+            if phase is None:
+                return r["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
+            if "alternating_bytes_per_launch" in r:
+                return r["alternating_bytes_per_launch"][phase], os.path.relpath(path, ROOT)
+    return None, None
+
+
 def roofline(cfg, B, size, layer_ms, frames=1):
     fam = cfg.get("family")
     if fam == "depth_pro":
@@ -150,7 +181,12 @@ def roofline(cfg, B, size, layer_ms, frames=1):
     breakdown = {c: {"ms": round(cls_ms[c], 4), "launches": cls_n[c],
                      "tflops": round(cls_fl[c] / (cls_ms[c] * 1e-3) / 1e12, 1) if cls_fl.get(c) else None}
                  for c in sorted(cls_ms, key=lambda c: -cls_ms[c])}
-    traffic, src = pmc_traffic(dom, cfg, B, size) if fam not in ("depth_pro", "vggt") else (None, None)
+    if fam == "vggt":
+        traffic, src = pmc_traffic_vggt(dom, cfg, B, frames)
+    elif fam != "depth_pro":
+        traffic, src = pmc_traffic(dom, cfg, B, size)
+    else:
+        traffic, src = None, None
     roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
             "flop_per_launch": per_launch_fl, "avg_launch_ms": round(avg_ms, 5),

@@ -77,7 +77,8 @@ __global__ void __launch_bounds__(NW * 64) gemm256_kernel(const GemmParams p) {
     const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
     bid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
   }
-  const int tm = bid / ntn, tn = bid - tm * ntn;
+  int tm, tn;
+  tile_of(bid, (p.M + BM - 1) / BM, ntn, tile_group_m(p.N, p.K), tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
   // glds geometry: a wave-instruction fills 8 rows x 128 B; lane -> (row lrow,

@@ -65,6 +65,31 @@ MDE_DEV int vt_pos(int t) {
   return (t & ~31) | ((k & 15) >> 2) << 3 | (k >> 4) << 2 | (k & 3);
 }
 
+// Tile (tm, tn) of the linear workgroup index `bid` (after the XCD remap,
+// which hands each XCD a contiguous run of bids).  gm <= 1: row-major, N
+// fastest -- the N tiles of a row block share A in one L2.  gm > 1: row
+// blocks in groups of gm, tm fastest inside a group, so the ~32 workgroups an
+// XCD runs together cover gm row blocks x a few N tiles and BOTH operands
+// stay L2-resident (W larger than an XCD's 4 MB L2 is otherwise re-streamed
+// once per row block).  Bijective for any ntm, ntn.
+MDE_DEV void tile_of(int bid, int ntm, int ntn, int gm, int& tm, int& tn) {
+  if (gm <= 1) {
+    tm = bid / ntn;
+    tn = bid - tm * ntn;
+    return;
+  }
+  const int per = gm * ntn;
+  const int g = bid / per, r = bid - g * per;
+  const int mb = g * gm;
+  const int gs = ntm - mb < gm ? ntm - mb : gm;
+  tn = r / gs;
+  tm = mb + (r - tn * gs);
+}
+
+// Row-block group of tile_of for a weight operand of n x k halves: group when
+// W would not stay resident in an XCD's L2 next to the A blocks.
+MDE_DEV int tile_group_m(int n, int k) { return (long long)n * k * 2 > (2ll << 20) ? 8 : 1; }
+
 MDE_DEV f16x8 zero8() {
   f16x8 z;
 #pragma unroll

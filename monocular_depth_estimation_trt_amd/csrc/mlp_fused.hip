@@ -220,12 +220,16 @@ bool mlp_fused_supported(int dim, int hidden, int ldw1, int ldw2) {
   return dim == D && hidden == HID && ldw1 == D && ldw2 == HID;
 }
 
-// MDE_FUSED_MLP: 0 never, 1 auto (default: enough 128-row blocks to fill the
-// chip at one workgroup per CU), 2 whenever supported.  Read per call (tests
-// toggle it between engines).
+// MDE_FUSED_MLP: 0 never (default), 1 auto (enough 128-row blocks to fill
+// the chip at one workgroup per CU), 2 whenever supported.  Read per call
+// (tests toggle it between engines).  Off by default: measured on MI355X at
+// B = 32 (profiles/r01_v12_dav2_layers_b32_fused.json) the fused launch takes
+// 0.246 ms against 0.207 ms for fc1 + fc2 -- with two stages in flight per
+// workgroup each 32 KB stage waits out a full L2 round trip (120 stages per
+// workgroup), so the kernel is load-latency bound at 420 TF/s.
 bool mlp_fused_enabled(int M) {
   const char* e = getenv("MDE_FUSED_MLP");
-  const int mode = e ? atoi(e) : 1;
+  const int mode = e ? atoi(e) : 0;
   if (mode == 0) return false;
   if (mode == 2) return true;
   return (M + BM - 1) / BM >= 256;

@@ -20,14 +20,25 @@ def collect(root):
         with open(f) as fh:
             for row in csv.DictReader(fh):
                 key = (row.get("Kernel_Name", ""), int(float(row.get("Grid_Size", 0) or 0)))
-                acc[key][row["Counter_Name"]].append(float(row["Counter_Value"]))
+                did = int(float(row.get("Dispatch_Id", 0) or 0))
+                acc[key][row["Counter_Name"]].append((did, float(row["Counter_Value"])))
+
+    def mean(v):
+        return sum(v) / max(1, len(v))
+
     out = []
     for (name, grid), d in acc.items():
-        f = sum(d.get("FETCH_SIZE", [0])) / max(1, len(d.get("FETCH_SIZE", [])))
-        w = sum(d.get("WRITE_SIZE", [0])) / max(1, len(d.get("WRITE_SIZE", [])))
-        out.append({"kernel": name, "grid": grid, "launches": len(d.get("FETCH_SIZE", [])),
-                    "fetch_kib": round(f, 1), "write_kib": round(w, 1),
-                    "hbm_bytes_per_launch": int((2 * f + w) * 1024)})
+        fs = [v for _, v in sorted(d.get("FETCH_SIZE", []))]
+        ws = [v for _, v in sorted(d.get("WRITE_SIZE", []))]
+        f, w = mean(fs), mean(ws)
+        rec = {"kernel": name, "grid": grid, "launches": len(fs),
+               "fetch_kib": round(f, 1), "write_kib": round(w, 1),
+               "hbm_bytes_per_launch": int((2 * f + w) * 1024)}
+        # two layers sharing one kernel + grid alternate in dispatch order
+        # (VGGT: attn.proj then mlp.fc2 per block): bytes of even / odd launches
+        if len(fs) >= 4 and len(ws) == len(fs):
+            rec["alternating_bytes_per_launch"] = [int((2 * mean(fs[i::2]) + mean(ws[i::2])) * 1024) for i in (0, 1)]
+        out.append(rec)
     out.sort(key=lambda r: -r["hbm_bytes_per_launch"] * max(1, r["launches"]))
     return out
 
