@@ -225,7 +225,7 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) 
     bid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
   }
   int tm, tn;
-  tile_of(bid, (p.M + BM - 1) / BM, ntn, AM == A_DENSE ? tile_group_m(p.N, p.K) : 1, tm, tn);
+  tile_of(bid, (p.M + BM - 1) / BM, ntn, AM == A_DENSE ? tile_group_m(p.N, p.K, BM) : 1, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
   // ---- glds lane geometry: lane -> (row within a wave-instruction, chunk)

@@ -78,7 +78,7 @@ __global__ void __launch_bounds__(NW * 64) gemm256_kernel(const GemmParams p) {
     bid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
   }
   int tm, tn;
-  tile_of(bid, (p.M + BM - 1) / BM, ntn, tile_group_m(p.N, p.K), tm, tn);
+  tile_of(bid, (p.M + BM - 1) / BM, ntn, tile_group_m(p.N, p.K, BM), tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
 
   // glds geometry: a wave-instruction fills 8 rows x 128 B; lane -> (row lrow,

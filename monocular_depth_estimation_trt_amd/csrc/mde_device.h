@@ -86,9 +86,19 @@ MDE_DEV void tile_of(int bid, int ntm, int ntn, int gm, int& tm, int& tn) {
   tm = mb + (r - tn * gs);
 }
 
-// Row-block group of tile_of for a weight operand of n x k halves: group when
-// W would not stay resident in an XCD's L2 next to the A blocks.
-MDE_DEV int tile_group_m(int n, int k) { return (long long)n * k * 2 > (2ll << 20) ? 8 : 1; }
+// Row-block group of tile_of for a weight operand of n x k halves and bm-row
+// tiles: group when W would not stay resident in an XCD's L2 next to the A
+// blocks, with at most ~2 MB of A rows per group.  Measured on VGGT-1B
+// (profiles/r01_v1[2-4]_vggt_traffic_*): qkv (K 1024, W 6 MB) 477 -> 222 MB
+// per launch with groups of 8; fc2 (K 4096, 1 MB of A per row block) best
+// row-major: 328 MB vs 344 (groups of 2) and 372 (groups of 8).
+MDE_DEV int tile_group_m(int n, int k, int bm) {
+  if ((long long)n * k * 2 <= (2ll << 20)) return 1;
+  const long long per = (long long)bm * k * 2;
+  if (per >= (1ll << 20)) return 1;
+  const int g = (int)((2ll << 20) / per);
+  return g < 1 ? 1 : (g > 8 ? 8 : g);
+}
 
 MDE_DEV f16x8 zero8() {
   f16x8 z;
