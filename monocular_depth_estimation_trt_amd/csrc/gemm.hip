@@ -206,7 +206,8 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) 
   constexpr int STAGE = (BM + BN) * ROWB;
   // dense A: SG-deep ring, every wave issues exactly NPER glds per stage so a
   // counted vmcnt names "stage kt has landed"
-  constexpr int SG = (AM == A_DENSE && AINS % NW == 0 && BINS % NW == 0) ? MDE_GEMM_STAGES : 2;
+  constexpr int SGMAX = 163840 / STAGE < MDE_GEMM_STAGES ? 163840 / STAGE : MDE_GEMM_STAGES;  // LDS limit
+  constexpr int SG = (AM == A_DENSE && AINS % NW == 0 && BINS % NW == 0 && SGMAX > 2) ? SGMAX : 2;
   constexpr int NPER = APASS + BPASS;
   static_assert(SG >= 2 && SG <= 4, "stages");
   __shared__ __attribute__((aligned(16))) char smem[SG * STAGE];
@@ -521,6 +522,19 @@ bool getenv_im2col() {
   return v != 0;
 }
 
+// Direct-conv tiles are 8 x 16 output pixels per image: on small maps most of
+// a tile is padding (19^2 -> 47 % useful).  The implicit-im2col GEMM tiles the
+// flattened B*oh*ow pixel axis instead, which wins for stride-2 convs and for
+// wide-K convs on maps that fill the 8 x 16 grid badly (MI355X, B=32: the
+// 37^2 -> 19^2 s2 384->384 conv 0.161 -> 0.069 ms, 19^2 384->64 0.047 ->
+// 0.042; narrow 64-channel convs stay direct: 0.015 vs 0.022).
+bool prefer_im2col(const GemmParams& p) {
+  if (p.amode != A_CONV3 || p.emode != E_STORE) return false;
+  if (p.stride == 2) return true;
+  const double tiles = (double)((p.oh + 7) / 8 * 8) * (double)((p.ow + 15) / 16 * 16);
+  return p.cc >= 256 && (double)p.oh * p.ow < 0.6 * tiles;
+}
+
 }  // namespace
 
 hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
@@ -532,7 +546,8 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
   if ((p.emode == E_STORE || p.emode == E_RESID || p.emode == E_PATCH) && (p.ldo & 7)) return hipErrorInvalidValue;
   if (p.emode == E_CONVT && (p.cout & 7)) return hipErrorInvalidValue;
   if (p.emode == E_HEAD && (p.N != 32 || p.amode == A_DENSE)) return hipErrorInvalidValue;
-  if (p.amode != A_DENSE && conv_direct_supported(p) && !getenv_im2col()) return launch_conv3(p, st);
+  if (p.amode != A_DENSE && conv_direct_supported(p) && !getenv_im2col() && !prefer_im2col(p))
+    return launch_conv3(p, st);
   if (p.ln_counter && (p.emode != E_RESID || (p.N != 384 && p.N != 768 && p.N != 1024) || p.ldo != p.N))
     return hipErrorInvalidValue;
   if (gemm256_eligible(p)) return launch_gemm256(p, st);
