@@ -21,6 +21,9 @@
 #ifndef MDE_EPI_LDS
 #define MDE_EPI_LDS 1  // row-major epilogue staged through LDS (whole-line stores)
 #endif
+#ifndef MDE_CONV_BRES
+#define MDE_CONV_BRES 1  // 32-wide convs with one channel chunk: all 9 weight taps LDS-resident (1: CK 32, 2: + CK 64)
+#endif
 
 namespace mde {
 
@@ -41,7 +44,12 @@ MDE_DEV int cpch(int pix, int lc) {
 
 constexpr int TH = 8, TW = 16;
 
-template <int BN, int WM, int WN, int CK, int S, bool UP, int EM>
+//
+// BRES (one channel chunk, p.cc == CK): the 9 weight taps (9 x BN x CK f16)
+// are staged once with the patch, so the tap loop runs without a barrier --
+// the head convs (32 output channels) otherwise pay 10 barriers for 36 MFMAs
+// per wave.
+template <int BN, int WM, int WN, int CK, int S, bool UP, int EM, bool BRES = false>
 __global__ void __launch_bounds__(WM * WN * 64) conv3_kernel(const GemmParams p) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int BM = TH * TW;
@@ -57,7 +65,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3_kernel(const GemmParams p)
   constexpr int BINS = BN / RWP;                              // B rows per wave-instruction = RWP
   static_assert(BINS * RWP == BN, "B tile rows");
   // the LDS-staged epilogue reuses the patch/B space for the fp32 tile
-  constexpr int MAIN = PATCH + 2 * BSTAGE, EPI = MDE_EPI_LDS ? BM * BN * 4 : 0;
+  constexpr int MAIN = PATCH + (BRES ? 9 : 2) * BSTAGE, EPI = MDE_EPI_LDS ? BM * BN * 4 : 0;
   __shared__ __attribute__((aligned(16))) char smem[MAIN > EPI ? MAIN : EPI];
   char* sP = smem;
   char* sB0 = smem + PATCH;
@@ -143,7 +151,42 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3_kernel(const GemmParams p)
 
   const int nchunk = p.cc / CK;
   const int nsteps = 9 * nchunk;
-  for (int chunk = 0; chunk < nchunk; ++chunk) {
+  if constexpr (BRES) {
+    load_patch(0);
+#pragma unroll
+    for (int t = 0; t < 9; ++t) load_b(t, t);
+    wait_vmc();
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+      const char* sB = sB0 + t * BSTAGE;
+      const int ky = t / 3, kx = t - (t / 3) * 3;
+#pragma unroll
+      for (int s = 0; s < CK / 32; ++s) {
+        const int lc = 4 * s + (lane >> 4);
+        f16x8 fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int pp = ((wm * TM + i) * S + ky) * PW + (lane & 15) * S + kx;
+          fa[i] = *reinterpret_cast<const f16x8*>(sP + pp * ROWB + cpch<CK>(pp, lc) * 16);
+          if constexpr (!UP) {
+            if (p.relu_in) fa[i] = relu8(fa[i]);
+          }
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int r = wn * TN * 16 + j * 16 + (lane & 15);
+          fb[j] = *reinterpret_cast<const f16x8*>(sB + r * ROWB + cpch<CK>(r, lc) * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);
+      }
+    }
+    __syncthreads();  // every wave done with the patch before the epilogue reuses the LDS
+  }
+  for (int chunk = 0; chunk < (BRES ? 0 : nchunk); ++chunk) {
     if (chunk > 0) __syncthreads();  // every wave done with the previous patch
     load_patch(chunk);
     const int step0 = chunk * 9;
@@ -208,8 +251,13 @@ hipError_t run_conv(const GemmParams& p, hipStream_t st) {
   const long long blocks =
       (long long)p.cb * ((p.oh + TH - 1) / TH) * ((p.ow + TW - 1) / TW) * ((p.N + BN - 1) / BN);
   if (blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL((conv3_kernel<BN, WM, WN, CK, S, UP, EM>), dim3((unsigned)blocks), dim3(WM * WN * 64), 0, st,
-                     p);
+  constexpr bool BRES_OK = BN == 32 && (CK == 32 ? MDE_CONV_BRES >= 1 : MDE_CONV_BRES >= 2);
+  if (BRES_OK && p.cc == CK)
+    hipLaunchKernelGGL((conv3_kernel<BN, WM, WN, CK, S, UP, EM, BRES_OK>), dim3((unsigned)blocks),
+                       dim3(WM * WN * 64), 0, st, p);
+  else
+    hipLaunchKernelGGL((conv3_kernel<BN, WM, WN, CK, S, UP, EM>), dim3((unsigned)blocks), dim3(WM * WN * 64), 0,
+                       st, p);
   return hipGetLastError();
 }
 
