@@ -63,7 +63,7 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--model", default="depth_anything_v2", choices=["depth_anything_v2", "depth_pro", "vggt"])
     p.add_argument("--batch", type=int, default=0,
-                   help="batch items per GPU per step (default 32; depth_pro 4; vggt 8)")
+                   help="batch items per GPU per step (default 30; depth_pro 4; vggt 8)")
     p.add_argument("--frames", type=int, default=1, help="vggt: frames per batch item (the packed S)")
     p.add_argument("--encoder", default="vits", choices=["vits", "vitb", "vitl"])
     p.add_argument("--size", type=int, default=518)
@@ -328,7 +328,10 @@ class Workload:
             from monocular_depth_estimation_trt_amd import pack, weights
             from monocular_depth_estimation_trt_amd.flops import total_flops
             self.S = S = a.size
-            self.B = B = a.batch or 32
+            # B=30 from the batch sweep (profiles/r01_v18_batch_sweep.json): at B=32
+            # the N=384 GEMMs make 1029 128x128 tiles for 1024 workgroup slots
+            # (256 CUs x 2), a third round of 5 tiles (proj 34 -> 41 us, fc2 67 -> 82 us)
+            self.B = B = a.batch or 30
             self.cfg = weights.model_config(a.encoder, "metric")
             self.sd = weights.synthetic_state_dict(self.cfg, 1234)
             self.blob = pack.pack_bytes(self.sd, self.cfg, S, S)
