@@ -236,6 +236,43 @@ hipError_t launch_depth_postprocess(const float* in, int B, int ih, int iw, floa
   return hipGetLastError();
 }
 
+namespace {
+// second half of the E_RESID split-K path (gemm.hip): one thread per 4
+// columns, slices added in order 0..S-1, then the E_RESID update
+__global__ void splitk_resid_kernel(const float* __restrict__ P, int S, int M, int N, const float* __restrict__ bias,
+                                    const float* __restrict__ ls, float* __restrict__ x32, int ldo) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int n4 = N >> 2;
+  if (i >= (long long)M * n4) return;
+  const int m = (int)(i / n4), n = (int)(i - (long long)m * n4) * 4;
+  const size_t plane = (size_t)M * N;
+  float4 a = *reinterpret_cast<const float4*>(P + (size_t)m * N + n);
+  for (int s = 1; s < S; ++s) {
+    const float4 b = *reinterpret_cast<const float4*>(P + s * plane + (size_t)m * N + n);
+    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
+  }
+  const float4 bn = bias ? *reinterpret_cast<const float4*>(bias + n) : float4{0.f, 0.f, 0.f, 0.f};
+  const float4 l = *reinterpret_cast<const float4*>(ls + n);
+  float4* x = reinterpret_cast<float4*>(x32 + (size_t)m * ldo + n);
+  float4 xv = *x;
+  xv.x += l.x * (a.x + bn.x);
+  xv.y += l.y * (a.y + bn.y);
+  xv.z += l.z * (a.z + bn.z);
+  xv.w += l.w * (a.w + bn.w);
+  *x = xv;
+}
+}  // namespace
+
+hipError_t launch_splitk_resid(const float* P, int S, int M, int N, const float* bias, const float* ls, float* x32,
+                               int ldo, hipStream_t st) {
+  if (S < 1 || (N & 3) || (ldo & 3) || !ls) return hipErrorInvalidValue;
+  const long long n = (long long)M * (N >> 2);
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(splitk_resid_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P, S, M, N, bias, ls,
+                     x32, ldo);
+  return hipGetLastError();
+}
+
 hipError_t launch_resize(const h16* in, h16* out, int B, int ih, int iw, int C, int oh, int ow, hipStream_t st) {
   if (C & 7) return hipErrorInvalidValue;
   const long long n = (long long)B * oh * ow * (C >> 3);

@@ -188,6 +188,7 @@ size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
   t.p2 = a.h(bb * s1 * F);
   t.c1 = a.h(bb * s0 * (F / 2));
   t.lncnt = (unsigned*)a.take((bb * e.T / 32 + 1) * 4);  // >= one word per 32-row block
+  t.ws = bb * e.T <= 4096 ? a.f(4 * bb * e.T * D) : nullptr;
   if (b) *b = t;
   return a.off;
 }
@@ -367,6 +368,14 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
       const bool tapped = tap < 4 && cf.taps[tap] == i;
       const std::string lg = pn + "ln1.g", lb = pn + "ln1.b";
       fuse_ln(g, i + 1 < cf.depth ? lg.c_str() : nullptr, lb.c_str(), tapped ? b.tap[tap] : nullptr);
+      // small batch: fc2's 64^2 tiles do not fill the chip and each walks a
+      // K = 4D loop -- split K four ways (B = 1 ViT-S: 132 -> 528 workgroups)
+      const long long t64 = (long long)((B * T + 63) / 64) * ((D + 63) / 64);
+      const char* sk = getenv("MDE_SPLITK");  // "0": off (A/B and tests; read per forward)
+      if (b.ws && !g.ln_counter && t64 < 256 && cf.mlp_hidden >= 1024 && !(sk && sk[0] == '0')) {
+        g.partial = b.ws;
+        g.splitk = 4;
+      }
       snprintf(nm, sizeof nm, "block%d.fc2", i);
       gemm(nm, g);
     }

@@ -34,6 +34,7 @@ struct DAV2Buf {
   h16 *tap[4], *pj[4], *l1, *l2, *l4, *rn[4];
   h16 *tb, *sb, *ub, *vb, *p4, *p3, *p2, *c1;
   unsigned* lncnt;  // fused-LayerNorm row-block arrival counters (zeroed, self-resetting)
+  float* ws;        // fc2 split-K partials [4][B*T][D] (small-batch contexts only, else null)
 };
 
 // Depth Pro activations (depth_pro.hip plan_arena_dp).  Token buffers are

@@ -298,9 +298,17 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) 
 
   f16x8 ru[UPC];
 
+  // K-tiles [kt0, kt0 + nk): all of K, or this workgroup's split-K slice
+  int nk = (p.K + BK - 1) / BK, kt0 = 0;
+  if constexpr (EM == E_PARTIAL) {
+    const int per = (nk + (int)gridDim.y - 1) / (int)gridDim.y;
+    kt0 = (int)blockIdx.y * per;
+    nk = min(nk - kt0, per);  // >= 1: the launcher uses at most nk slices of ceil(nk / S) tiles
+  }
+
   auto issue = [&](int kt, int buf) {
     char* sbase = smem + buf * STAGE;
-    const int k0 = kt * BK;
+    const int k0 = (kt + kt0) * BK;
 #pragma unroll
     for (int i = 0; i < BPASS; ++i)
       if (BINS % NW == 0 || wave + i * NW < BINS)
@@ -371,7 +379,6 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) 
 #pragma unroll
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = (p.K + BK - 1) / BK;
   auto mma_stage = [&](int cur) {
     const char* sA = smem + cur * STAGE;
     const char* sB = sA + BM * ROWB;
@@ -550,6 +557,26 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
     return launch_conv3(p, st);
   if (p.ln_counter && (p.emode != E_RESID || (p.N != 384 && p.N != 768 && p.N != 1024) || p.ldo != p.N))
     return hipErrorInvalidValue;
+  if (p.emode == E_RESID && p.splitk > 1 && p.partial && !p.ln_counter && p.amode == A_DENSE) {
+    // small M, long K (B = 1 fc2: 132 64^2 tiles x 24 K-steps): S slices of
+    // the K loop fill the chip, a second kernel adds them in slice order
+    const int nk = (p.K + 63) / 64;
+    int S = p.splitk < nk ? p.splitk : nk;
+    const int per = (nk + S - 1) / S;
+    S = (nk + per - 1) / per;  // every slice non-empty
+    GemmParams q = p;
+    q.emode = E_PARTIAL;
+    q.x32 = p.partial;
+    q.ldo = p.N;
+    q.bias = nullptr;
+    q.ls = nullptr;
+    const unsigned tiles = (unsigned)(((p.M + 63) / 64) * ((p.N + 63) / 64));
+    hipLaunchKernelGGL((gemm_kernel<64, 64, MDE_GEMM_BK, 2, 2, A_DENSE, E_PARTIAL>), dim3(tiles, (unsigned)S),
+                       dim3(256), 0, st, q);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return launch_splitk_resid(p.partial, S, p.M, p.N, p.bias, p.ls, p.x32, p.ldo, st);
+  }
   if (gemm256_eligible(p)) return launch_gemm256(p, st);
   if (p.amode == A_DENSE && gemm_persistent_enabled() && !p.ln_counter) {
     // one 256x128 tile per CU per round at least: the persistent pipeline wins

@@ -21,7 +21,8 @@ enum EMode : int {
   E_RESID = 2,   // x32[m*ldo+n] += ls[n] * (acc + bias[n])
   E_PATCH = 3,   // x32[(b*T+tok0+p)*ldo+n] = acc + bias[n] + pos[p*ldo+n]
   E_CONVT = 4,   // ConvTranspose(k=s) pixel-shuffle store into NHWC f16
-  E_HEAD = 5     // relu(acc+bias(+pe)) . w2 + b2 -> sigmoid*max | relu | exp -> fp32 map
+  E_HEAD = 5,    // relu(acc+bias(+pe)) . w2 + b2 -> sigmoid*max | relu | exp -> fp32 map
+  E_PARTIAL = 6  // split-K slice blockIdx.y: x32[y*M*ldo + m*ldo + n] = acc (internal to the E_RESID split path)
 };
 
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };
@@ -65,7 +66,16 @@ struct GemmParams {
   float ln_eps = 1e-6f; int ln_T = 1;
   const float *ln1_g = nullptr, *ln1_b = nullptr; h16* ln1_out = nullptr; int ln1_skip = 0;
   const float *ln2_g = nullptr, *ln2_b = nullptr; h16* ln2_out = nullptr; int ln2_skip = 0;
+  // E_RESID split-K (small M, long K): splitk > 1 and partial = fp32
+  // workspace [splitk][M][N]; the K range is cut into splitk slices whose
+  // partial sums are added in slice order by a second kernel (deterministic)
+  int splitk = 1; float* partial = nullptr;
 };
+
+// x32[m*ldo+n] += ls[n] * (sum_{s<S} P[s][m][n] + bias[n]), slices summed in
+// order (elementwise.hip): the second half of the E_RESID split-K path
+hipError_t launch_splitk_resid(const float* P, int S, int M, int N, const float* bias, const float* ls, float* x32,
+                               int ldo, hipStream_t st);
 
 hipError_t launch_gemm(const GemmParams& p, hipStream_t st);
 

@@ -46,6 +46,17 @@ MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&m
       }
     }
     return;
+  } else if constexpr (EM == E_PARTIAL) {
+    float* dst = p.x32 + (size_t)blockIdx.y * p.M * p.ldo;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int n = ncol + j * 16;
+      if (n >= p.N) continue;
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+        if (mrow[i] >= 0) *reinterpret_cast<f32x4*>(dst + (size_t)mrow[i] * p.ldo + n) = acc[i][j];
+    }
+    return;
   } else {
 #pragma unroll
     for (int j = 0; j < TN; ++j) {

@@ -126,3 +126,24 @@ def test_batch_and_graph_consistency(gpu):
         yi = run_engine(blob, x[i:i + 1], max_batch=4)
         m = depth_metrics(yi, y3[i:i + 1])
         assert m["max_abs"] < 0.05 and m["rel_mean"] < 1e-3, (i, m)
+
+
+def test_fc2_splitk_matches_unsplit(gpu):
+    """Small-batch contexts split fc2's K loop four ways (engine.hip, fc2);
+    the slices are summed in order, so the result is deterministic and equal
+    to the unsplit GEMM up to fp32 reassociation."""
+    import os
+    cfg = weights.model_config("vits", "metric")
+    sd = weights.synthetic_state_dict(cfg, 5)
+    blob = pack.pack_bytes(sd, cfg, 98, 98)
+    x = weights.synthetic_images(1, 98, 98, first_seed=21)
+    y_split = run_engine(blob, x, graph=True)
+    assert np.array_equal(y_split, run_engine(blob, x, graph=False)), "split-K must be deterministic"
+    os.environ["MDE_SPLITK"] = "0"
+    try:
+        y_plain = run_engine(blob, x)
+    finally:
+        os.environ.pop("MDE_SPLITK", None)
+    m = depth_metrics(y_split, y_plain)
+    print("split-K vs unsplit", m)
+    assert m["max_abs"] < 0.05 and m["rel_mean"] < 1e-3, m

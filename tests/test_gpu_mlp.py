@@ -73,12 +73,14 @@ def test_engine_fused_mlp_equals_unfused(gpu):
     x = weights.synthetic_images(2, 98, 98, first_seed=100)
     blob = pack.pack_bytes(sd, cfg, 98, 98)
     outs = {}
+    os.environ["MDE_SPLITK"] = "0"  # compare against the plain (unsplit) fc2
     for mode in ("0", "2"):
         os.environ["MDE_FUSED_MLP"] = mode
         try:
             outs[mode] = _run(blob, x)
         finally:
             os.environ.pop("MDE_FUSED_MLP", None)
+    os.environ.pop("MDE_SPLITK", None)
     d = float(np.abs(outs["0"] - outs["2"]).max())
     print("fused vs unfused max_abs", d)
     assert np.isfinite(outs["2"]).all()
