@@ -295,6 +295,18 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
   for (int i = 0; i < cf.depth; ++i) {
     const std::string p = "b" + std::to_string(i) + ".";
     const std::string pn = "b" + std::to_string(i + 1) + ".";
+    // small batch: fc2's 64^2 tiles do not fill the chip and each walks a
+    // K = 4D loop -- split K (B = 1: ViT-S 132 tiles x 4, ViT-L 352 x 2;
+    // ViT-L fc2 1.23 -> 0.88 ms per forward; proj at K = 1024 gained
+    // nothing); MDE_SPLITK=0 turns it off (A/B, tests)
+    auto split_k = [&](GemmParams& g, int K) {
+      const long long t64 = (long long)((B * T + 63) / 64) * ((D + 63) / 64);
+      const char* sk = getenv("MDE_SPLITK");
+      if (b.ws && !g.ln_counter && t64 < 512 && K >= 1024 && !(sk && sk[0] == '0')) {
+        g.partial = b.ws;
+        g.splitk = t64 < 256 ? 4 : 2;
+      }
+    };
     if (!fuse || i == 0) {
       snprintf(nm, sizeof nm, "block%d.norm1", i);
       step(nm, [&] {
@@ -368,14 +380,7 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
       const bool tapped = tap < 4 && cf.taps[tap] == i;
       const std::string lg = pn + "ln1.g", lb = pn + "ln1.b";
       fuse_ln(g, i + 1 < cf.depth ? lg.c_str() : nullptr, lb.c_str(), tapped ? b.tap[tap] : nullptr);
-      // small batch: fc2's 64^2 tiles do not fill the chip and each walks a
-      // K = 4D loop -- split K four ways (B = 1 ViT-S: 132 -> 528 workgroups)
-      const long long t64 = (long long)((B * T + 63) / 64) * ((D + 63) / 64);
-      const char* sk = getenv("MDE_SPLITK");  // "0": off (A/B and tests; read per forward)
-      if (b.ws && !g.ln_counter && t64 < 256 && cf.mlp_hidden >= 1024 && !(sk && sk[0] == '0')) {
-        g.partial = b.ws;
-        g.splitk = 4;
-      }
+      split_k(g, cf.mlp_hidden);
       snprintf(nm, sizeof nm, "block%d.fc2", i);
       gemm(nm, g);
     }
