@@ -66,6 +66,8 @@ struct VGBuf {
   h16* tap;                // LN(cat(frame, global)) patch tokens [n*np][2D]
   h16 *pj[4], *l1, *l2, *l4, *rn[4];
   h16 *tb, *sb, *ub, *vb, *p4, *p3, *p2, *c1;
+  float* ws;               // fc2 split-K partials [4][ws_rows][D] (small-batch contexts only, else null)
+  size_t ws_rows;
 };
 
 enum Family : int { FAMILY_DAV2 = 0, FAMILY_DEPTH_PRO = 1, FAMILY_VGGT = 2 };

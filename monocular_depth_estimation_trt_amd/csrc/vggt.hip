@@ -25,6 +25,7 @@
 // (global, separate buffers when S > 1); maps NHWC f16 over the B*S frames.
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <initializer_list>
 
 #include "engine_internal.h"
@@ -165,6 +166,8 @@ size_t plan_arena_vggt(const mde_engine& e, int B, VGBuf* b, uint8_t* base) {
   t.p3 = a.h(n * s2 * F);
   t.p2 = a.h(n * s1 * F);
   t.c1 = a.h(n * s0 * (F / 2));
+  t.ws_rows = n * T <= 4096 ? n * T : 0;
+  t.ws = t.ws_rows ? a.f(4 * t.ws_rows * D) : nullptr;
   if (b) *b = t;
   return a.off;
 }
@@ -236,6 +239,14 @@ void Runner::vggt_block(const std::string& p, float eps, bool qk, int seqs, int 
     g.ls = w32(p + "ls2");
     g.x32 = v.X;
     g.ldo = D;
+    // small batch: split fc2's K = 4D loop (as the DA-V2 fc2, engine.hip);
+    // B = 1, S = 1: 352 64^2 tiles x 2 slices
+    const long long t64 = (long long)((rows + 63) / 64) * ((D + 63) / 64);
+    const char* sk = getenv("MDE_SPLITK");
+    if (v.ws && (size_t)rows <= v.ws_rows && t64 < 512 && mlp >= 1024 && !(sk && sk[0] == '0')) {
+      g.partial = v.ws;
+      g.splitk = t64 < 256 ? 4 : 2;
+    }
     gemm((p + "fc2").c_str(), g);
   }
 }
