@@ -139,10 +139,19 @@ __global__ void __launch_bounds__(256) depth_post_kernel(const float* __restrict
   const long long n = (long long)B * oh * ow;
   const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (id >= n) return;
-  const int ox = (int)(id % ow);
-  const long long q = id / ow;
-  const int oy = (int)(q % oh);
-  const int b = (int)(q / oh);
+  int ox, oy, b;
+  if (n < (1LL << 31)) {  // 32-bit index split (see resize_kernel)
+    unsigned u = (unsigned)id;
+    ox = (int)(u % (unsigned)ow);
+    u /= (unsigned)ow;
+    oy = (int)(u % (unsigned)oh);
+    b = (int)(u / (unsigned)oh);
+  } else {
+    ox = (int)(id % ow);
+    const long long q = id / ow;
+    oy = (int)(q % oh);
+    b = (int)(q / oh);
+  }
   int y0, y1, x0, x1;
   float ly0, ly1, lx0, lx1;
   ac_index(ac_scale(ih, oh), oy, ih, y0, y1, ly0, ly1);
@@ -161,12 +170,23 @@ __global__ void __launch_bounds__(256) resize_kernel(const f16* __restrict__ in,
   const long long n = (long long)B * oh * ow * C8;
   const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (id >= n) return;
-  const int c8 = (int)(id % C8);
-  long long pix = id / C8;
-  const int ox = (int)(pix % ow);
-  pix /= ow;
-  const int oy = (int)(pix % oh);
-  const int b = (int)(pix / oh);
+  int c8, ox, oy, b;
+  if (n < (1LL << 31)) {  // 32-bit index split: a 64-bit divide is a long emulated sequence
+    unsigned u = (unsigned)id;
+    c8 = (int)(u % (unsigned)C8);
+    u /= (unsigned)C8;
+    ox = (int)(u % (unsigned)ow);
+    u /= (unsigned)ow;
+    oy = (int)(u % (unsigned)oh);
+    b = (int)(u / (unsigned)oh);
+  } else {
+    c8 = (int)(id % C8);
+    long long pix = id / C8;
+    ox = (int)(pix % ow);
+    pix /= ow;
+    oy = (int)(pix % oh);
+    b = (int)(pix / oh);
+  }
   int y0, y1, x0, x1;
   float ly0, ly1, lx0, lx1;
   ac_index(ac_scale(ih, oh), oy, ih, y0, y1, ly0, ly1);
