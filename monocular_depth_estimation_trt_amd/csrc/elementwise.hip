@@ -62,11 +62,21 @@ __global__ void __launch_bounds__(256) patch_prep_kernel(const float* __restrict
   const long long nchunk = (long long)B * np * 84;  // 3 channels x 14 rows x 2 halves
   long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (id < nchunk) {
-    const long long patch = id / 84;
-    const int r = (int)(id - patch * 84);
+    long long patch;
+    int r, b, pi;
+    if (nchunk < (1LL << 31)) {  // 32-bit index split (a 64-bit divide is emulated)
+      const unsigned u = (unsigned)id, pu = u / 84u;
+      patch = pu;
+      r = (int)(u - pu * 84u);
+      b = (int)(pu / (unsigned)np);
+      pi = (int)(pu - (unsigned)b * (unsigned)np);
+    } else {
+      patch = id / 84;
+      r = (int)(id - patch * 84);
+      b = (int)(patch / np);
+      pi = (int)(patch - (long long)b * np);
+    }
     const int c = r / 28, ky = (r % 28) >> 1, half = r & 1;
-    const int b = (int)(patch / np);
-    const int pi = (int)(patch - (long long)b * np);
     const int py = pi / pw, px = pi - (pi / pw) * pw;
     const float* src = img + (((size_t)b * 3 + c) * H + py * 14 + ky) * W + px * 14 + half * 8;
     f16x8 v;
