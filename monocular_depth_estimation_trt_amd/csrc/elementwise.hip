@@ -53,6 +53,10 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
   }
 }
 
+#ifndef MDE_RESIZE_F16
+#define MDE_RESIZE_F16 1  // NHWC f16 resize blend in packed f16 (0: fp32 blend, A/B)
+#endif
+
 constexpr int PK = 3 * 14 * 16;  // patch row length (K of the patch-embed GEMM)
 
 __global__ void __launch_bounds__(256) patch_prep_kernel(const float* __restrict__ img, f16* __restrict__ P,
@@ -207,9 +211,23 @@ __global__ void __launch_bounds__(256) resize_kernel(const f16* __restrict__ in,
   const f16x8 c = *reinterpret_cast<const f16x8*>(base + ((size_t)y1 * iw + x0) * C);
   const f16x8 d = *reinterpret_cast<const f16x8*>(base + ((size_t)y1 * iw + x1) * C);
   f16x8 v;
+#if MDE_RESIZE_F16
+  // packed f16 blend, as the up-conv staging (conv.hip) and TensorRT's fp16 Resize
+  typedef f16 f16x2r __attribute__((ext_vector_type(2)));
+  const f16x2r wx0 = {(f16)lx0, (f16)lx0}, wx1 = {(f16)lx1, (f16)lx1};
+  const f16x2r wy0 = {(f16)ly0, (f16)ly0}, wy1 = {(f16)ly1, (f16)ly1};
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const f16x2r a2 = {a[j], a[j + 1]}, b2 = {bb[j], bb[j + 1]}, c2 = {c[j], c[j + 1]}, d2 = {d[j], d[j + 1]};
+    const f16x2r r = (a2 * wx0 + b2 * wx1) * wy0 + (c2 * wx0 + d2 * wx1) * wy1;
+    v[j] = r[0];
+    v[j + 1] = r[1];
+  }
+#else
 #pragma unroll
   for (int j = 0; j < 8; ++j)
     v[j] = (f16)(ly0 * (lx0 * (float)a[j] + lx1 * (float)bb[j]) + ly1 * (lx0 * (float)c[j] + lx1 * (float)d[j]));
+#endif
   *reinterpret_cast<f16x8*>(out + (size_t)id * 8) = v;
 }
 
