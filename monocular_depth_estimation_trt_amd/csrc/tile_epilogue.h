@@ -174,9 +174,14 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
   constexpr int CPR = C / 8;               // lanes per row in the read-back (8 columns each)
   constexpr int RPI = 64 / CPR;            // rows per read-back instruction
   static_assert(TN >= 1 && C % 8 == 0, "tile");
-  if constexpr (EM != E_STORE && EM != E_RESID && EM != E_QKV) {
+  if constexpr (EM != E_STORE && EM != E_RESID && EM != E_QKV && EM != E_CONVT) {
     return false;
   } else {
+    // E_CONVT: 8 consecutive columns stay inside one sub-pixel when cout % 8 == 0,
+    // so each lane writes 16 B of one output pixel (the direct path writes 8 B)
+    if constexpr (EM == E_CONVT) {
+      if (p.cout & 7) return false;
+    }
     int which = 0;
     if constexpr (EM == E_QKV) {
       which = n0w / (p.heads * 64);
@@ -188,7 +193,7 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
     for (int j = 0; j < TN; ++j) {
       const int n = n0w + j * 16 + (lane >> 4) * 4;
       float4 bn = {0.f, 0.f, 0.f, 0.f};
-      if (p.bias && n < p.N) bn = *reinterpret_cast<const float4*>(p.bias + n);
+      if (p.bias && n < p.N) bn = *reinterpret_cast<const float4*>(p.bias + (EM == E_CONVT ? n % p.cout : n));
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         f32x4 v = acc[i][j];
@@ -255,6 +260,18 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
         x1.x += ls1.x * v[4]; x1.y += ls1.y * v[5]; x1.z += ls1.z * v[6]; x1.w += ls1.w * v[7];
         x[0] = x0;
         x[1] = x1;
+      } else if constexpr (EM == E_CONVT) {
+        const int q = n / p.cout, co = n - q * p.cout;
+        const int dy = q / p.s, dx = q - (q / p.s) * p.s;
+        const int hw = p.ih * p.iw;
+        const int b = m / hw, rem = m - (m / hw) * hw;
+        const int y = rem / p.iw, x = rem - (rem / p.iw) * p.iw;
+        const int OH = p.ih * p.s, OW = p.iw * p.s;
+        const size_t o = (((size_t)b * OH + y * p.s + dy) * OW + x * p.s + dx) * p.ldo + co;
+        f16x8 h;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) h[r] = (f16)v[r];
+        *reinterpret_cast<f16x8*>(reinterpret_cast<f16*>(p.out16) + o) = h;
       } else {  // E_QKV, q or k third
         const int D = p.heads * 64, w = n - which * D;
         const int b = m / p.T, t = m - (m / p.T) * p.T;
