@@ -2,18 +2,23 @@
 """Depth Anything V2 throughput on MI355X through the HIP engine.
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--encoder vits]
+    python bench.py --gpus 8 --encoder vitl --global-batch 8   (BASELINE config 3)
     python bench.py --model depth_pro [--batch 4]     (SURVEY.md 8f row 3, 1536^2)
     python bench.py --model vggt [--batch 8] [--frames 1]   (SURVEY.md 8f row 4, 518^2)
 
 One *step* = one forward of the packed DA-V2 engine over one batch of B
 synthetic 518x518 images already resident in HBM (input fp32 NCHW, output
 fp32 depth), enqueued on one HIP stream, replayed from the engine's
-captured hipGraph.  N > 1: one process per GPU (torch.distributed.run),
-each rank an independent replica on its own batch shard -- no collective on
-the data path; a gloo barrier brackets the timed region and
-the max time over ranks is used.  `value` = images processed by all ranks /
-that time (weak scaling: per-GPU batch fixed).  VGGT counts frames: a batch
-item of S frames is S images.
+captured hipGraph.  N > 1: one process per GPU, each rank an independent
+replica on its own batch shard -- no collective on the data path (SURVEY.md
+8e); a gloo barrier brackets the timed region and the max time over ranks is
+used.  Launched either by torch.distributed.run (RANK / WORLD_SIZE set) or
+directly: `python bench.py --gpus N` spawns the N rank processes itself
+(replicas.spawn_local) before anything touches the GPU.  `value` = images
+processed by all ranks / that time.  Default: weak scaling (`--batch` images
+per GPU); `--global-batch G` shards G images over the ranks instead (strong
+scaling, replicas.shard: config 3 = ViT-L, G = 8).  VGGT counts frames: a
+batch item of S frames is S images.
 
 Also measured (rank 0):
   * b1_*: the reference's own methodology (core/bench.py:182-210): batch 1,
@@ -25,7 +30,13 @@ Also measured (rank 0):
   * roofline: the dominant layer class (largest share of forward time), its
     algorithmic FLOP per launch / its average launch time, timed live with
     hipEvents on the engine's stream (the engine profiler), vs the dense
-    fp16 MFMA peak (2.5 PF/s, MI355X_MICROARCH.md).
+    fp16 MFMA peak (2.5 PF/s, MI355X_MICROARCH.md); `traffic` = that class's
+    HBM bytes per launch from the committed per-layer PMC profile of this
+    workload (tools/profile_round.sh -> profiles/traffic_*.json).
+  * vs_baseline: null -- BASELINE.md publishes no number for this metric
+    (HBM-resident throughput); the like-for-like ratio is b1_vs_ref_fps
+    (batch 1, PCIe-inclusive, the reference's method) and
+    throughput_vs_ref_b1 = value / 232.11 says how far batching goes.
   * cpu_baseline (N == 1 only): the oracle's fp32 CPU forward (a PyTorch
     restatement of upstream DA-V2) on this host's cores, bounded sample.
 """
@@ -56,14 +67,16 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--model", default="depth_anything_v2", choices=["depth_anything_v2", "depth_pro", "vggt"])
     p.add_argument("--batch", type=int, default=0,
-                   help="batch items per GPU per step (default 30; depth_pro 4; vggt 8)")
+                   help="batch items per GPU per step (default 28; depth_pro 4; vggt 8)")
+    p.add_argument("--global-batch", type=int, default=0,
+                   help="shard this many items over the ranks instead (strong scaling; config 3: 8)")
     p.add_argument("--frames", type=int, default=1, help="vggt: frames per batch item (the packed S)")
     p.add_argument("--encoder", default="vits", choices=["vits", "vitb", "vitl"])
     p.add_argument("--size", type=int, default=518)
@@ -74,7 +87,7 @@ def parse():
     p.add_argument("--no-b1", action="store_true")
     p.add_argument("--profile-iters", type=int, default=3)
     p.add_argument("--layers-json", default="", help="write the per-layer profile here (rank 0)")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
 class LayerTimes:
@@ -97,63 +110,27 @@ def profile_layers(ctx, stream, iters):
     return {k: statistics.median(v) for k, v in prof.ms.items()}
 
 
-# layer class -> kernel symbol substring in rocprofv3 traces (classes whose
-# launches map to one kernel template; GEMM classes share gemm_kernel<...>)
-CLASS_KERNEL = {"attn": "attn_fwd_kernel"}
+def traffic_path(model, encoder, B, size, frames=1):
+    tag = f"{model}_{encoder}_b{B}_{size}" + (f"_s{frames}" if model == "vggt" else "")
+    return os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
 
 
-def pmc_traffic(cls, cfg, B, size):
-    """HBM bytes per launch of the dominant class's kernel from the committed
-    PMC profile of this workload (tools/profile_round.sh -> profiles/
-    traffic_<enc>_b<B>.json: FETCH_SIZE x2 + WRITE_SIZE, separate passes), or
-    None.  Attention is matched by kernel name and grid size."""
-    path = os.path.join(ROOT, "profiles", f"traffic_{cfg['encoder']}_b{B}_{size}.json")
-    sub = CLASS_KERNEL.get(cls)
-    if not sub or not os.path.exists(path):
-        return None, None
-    with open(path) as f:
-        d = json.load(f)
-    grid = None
-    if cls == "attn":
-        grid = ((1370 if size == 518 else (size // 14) ** 2 + 1) + 127) // 128 * B * cfg["num_heads"] * 512
-    for r in d["kernels"]:
-        if sub in r["kernel"] and (grid is None or r["grid"] == grid):
-            return r["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
-    return None, None
-
-
-def pmc_traffic_vggt(cls, cfg, B, frames):
-    """VGGT: HBM bytes per launch of the dominant class's kernel from
-    profiles/traffic_vggt_b<B>_s<S>.json.  Token-major GEMMs are matched by
-    template + grid (work-items); proj and fc2 share the 128^2 E_RESID GEMM
-    and alternate in dispatch order (proj first in every block)."""
-    import re
-    path = os.path.join(ROOT, "profiles", f"traffic_vggt_b{B}_s{frames}.json")
+def pmc_traffic(layer_names, path):
+    """HBM bytes per launch of a layer class from the committed per-layer
+    PMC profile (tools/pmc_traffic.py: FETCH_SIZE x2 + WRITE_SIZE per
+    dispatch, separate passes, dispatches matched to the engine's layer order),
+    averaged over the class's layers; None when no profile covers them."""
     if not os.path.exists(path):
-        return None, None
-    T = (cfg["img"] // cfg["patch"]) ** 2 + 5
-    M, D = B * frames * T, cfg["embed_dim"]
-    layer = cls.split(".")[-1]
-    if layer in ("proj", "fc2"):
-        pat, grid = r"gemm_kernel<128, 128, 64, 2, 2, 0, 2>", -(-M // 128) * -(-D // 128) * 256
-        phase = 0 if layer == "proj" else 1
-    elif layer == "attn":
-        seqs, L = (B, frames * T) if cls.startswith("gb") else (B * frames, T)
-        pat, grid, phase = r"attn_fwd_kernel", -(-L // 128) * seqs * cfg["num_heads"] * 512, None
-    else:
-        return None, None
+        return None
     with open(path) as f:
-        d = json.load(f)
-    for r in d["kernels"]:
-        if re.search(pat, r["kernel"]) and r["grid"] == grid:
-            if phase is None:
-                return r["hbm_bytes_per_launch"], os.path.relpath(path, ROOT)
-            if "alternating_bytes_per_launch" in r:
-                return r["alternating_bytes_per_launch"][phase], os.path.relpath(path, ROOT)
-    return None, None
+        layers = json.load(f).get("layers", {})
+    got = [layers[n]["hbm_bytes_per_launch"] for n in layer_names if n in layers]
+    if not got or len(got) != len(layer_names):
+        return None
+    return int(sum(got) / len(got))
 
 
-def roofline(cfg, B, size, layer_ms, frames=1):
+def roofline(cfg, B, size, layer_ms, frames=1, traffic_file=""):
     fam = cfg.get("family")
     if fam == "depth_pro":
         from monocular_depth_estimation_trt_amd import flops_depth_pro as flops
@@ -164,10 +141,6 @@ def roofline(cfg, B, size, layer_ms, frames=1):
     else:
         from monocular_depth_estimation_trt_amd import flops
         lf = flops.layer_flops(cfg, size, size, B)
-    for name in layer_ms:
-        if name.endswith(".mlp") and name not in lf:   # fused fc1 + GELU + fc2 (csrc/mlp_fused.hip)
-            base = name[:-len(".mlp")]
-            lf[name] = lf.get(base + ".fc1", 0.0) + lf.get(base + ".fc2", 0.0)
     cls_ms, cls_fl, cls_n = {}, {}, {}
     for name, ms in layer_ms.items():
         c = flops.layer_class(name)
@@ -181,19 +154,14 @@ def roofline(cfg, B, size, layer_ms, frames=1):
     breakdown = {c: {"ms": round(cls_ms[c], 4), "launches": cls_n[c],
                      "tflops": round(cls_fl[c] / (cls_ms[c] * 1e-3) / 1e12, 1) if cls_fl.get(c) else None}
                  for c in sorted(cls_ms, key=lambda c: -cls_ms[c])}
-    if fam == "vggt":
-        traffic, src = pmc_traffic_vggt(dom, cfg, B, frames)
-    elif fam != "depth_pro":
-        traffic, src = pmc_traffic(dom, cfg, B, size)
-    else:
-        traffic, src = None, None
+    traffic = pmc_traffic([n for n in layer_ms if flops.layer_class(n) == dom], traffic_file)
     roof = {"bound": "mfma", "kernel": dom, "achieved": round(achieved, 2), "peak": MFMA_PEAK_TFLOPS,
             "unit": "TFLOP/s", "frac": round(achieved / MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
             "flop_per_launch": per_launch_fl, "avg_launch_ms": round(avg_ms, 5),
             "launches_per_step": cls_n[dom]}
     if traffic is not None:
         roof["traffic_unit"] = "bytes/launch"
-        roof["traffic_source"] = src
+        roof["traffic_source"] = os.path.relpath(traffic_file, ROOT)
     return roof, breakdown
 
 
@@ -282,7 +250,9 @@ def cpu_baseline(cfg, size, seconds):
 class Workload:
     """The packed engine, its io tensors and the constants of one bench model."""
 
-    def __init__(self, a, rank):
+    def __init__(self, a, B, first):
+        """B items on this rank (0: an idle rank of a strong-scaling run),
+        synthetic item seeds from `first` on."""
         import torch
         self.frames = 1
         self.input_name = "input"
@@ -292,7 +262,7 @@ class Workload:
             from monocular_depth_estimation_trt_amd.flops_depth_pro import total_flops
             self.cfg = WD.depth_pro_config("dinov2l16_384")
             self.S = S = self.cfg["img"]
-            self.B = B = a.batch or 4
+            self.B = B
             self.sd = WD.synthetic_state_dict(self.cfg, 4321)
             self.blob = PD.pack_bytes(self.sd, self.cfg)
             self.images = lambda n, seed: WD.synthetic_images(n, S, first_seed=seed)  # noqa: E731
@@ -301,7 +271,7 @@ class Workload:
             self.ref_fps = REF_DP_B1_FPS
             self.label = "Depth Pro"
             self.workload = (f"Depth Pro (3 x DINOv2-L/16 at 384^2, 35-patch pyramid, FOV head) {S}x{S}, forward, "
-                             f"batch {B} per GPU, inputs resident in HBM, hipGraph replay")
+                             f"{a.per_gpu_desc}, inputs resident in HBM, hipGraph replay")
             self.weights = "synthetic seeded (seed 4321), fan-in scaled"
             self.encoder = "dinov2l16_384"
         elif a.model == "vggt":
@@ -310,7 +280,7 @@ class Workload:
             from monocular_depth_estimation_trt_amd.flops_vggt import total_flops
             self.cfg = WV.vggt_config("vggt_1b")
             self.S = S = self.cfg["img"]
-            self.B = B = a.batch or 8
+            self.B = B
             self.frames = Fr = a.frames
             self.input_name = "images"
             self.sd = WV.synthetic_state_dict(self.cfg, 2468)
@@ -321,17 +291,14 @@ class Workload:
             self.ref_fps = REF_VGGT_B1_FPS
             self.label = "VGGT-1B depth"
             self.workload = (f"VGGT-1B depth path (DINOv2-L/14-reg + 24 frame/global block pairs + DPT) {S}x{S}, "
-                             f"S={Fr} frames, forward, batch {B} per GPU, inputs resident in HBM, hipGraph replay")
+                             f"S={Fr} frames, forward, {a.per_gpu_desc}, inputs resident in HBM, hipGraph replay")
             self.weights = "synthetic seeded (seed 2468), fan-in scaled"
             self.encoder = "vggt_1b"
         else:
             from monocular_depth_estimation_trt_amd import pack, weights
             from monocular_depth_estimation_trt_amd.flops import total_flops
             self.S = S = a.size
-            # B=30 from the batch sweep (profiles/r01_v18_batch_sweep.json): at B=32
-            # the N=384 GEMMs make 1029 128x128 tiles for 1024 workgroup slots
-            # (256 CUs x 2), a third round of 5 tiles (proj 34 -> 41 us, fc2 67 -> 82 us)
-            self.B = B = a.batch or 30
+            self.B = B
             self.cfg = weights.model_config(a.encoder, "metric")
             self.sd = weights.synthetic_state_dict(self.cfg, 1234)
             self.blob = pack.pack_bytes(self.sd, self.cfg, S, S)
@@ -340,12 +307,13 @@ class Workload:
             self.gflop = total_flops(self.cfg, S, S) / 1e9
             self.ref_fps = REF_B1_FPS
             self.label = f"DA-V2 {ENC_LABEL.get(a.encoder, a.encoder)}"
-            self.workload = (f"Depth Anything V2 {a.encoder} {S}x{S} metric head, forward, batch {B} per GPU, "
+            self.workload = (f"Depth Anything V2 {a.encoder} {S}x{S} metric head, forward, {a.per_gpu_desc}, "
                              f"inputs resident in HBM, hipGraph replay")
             self.weights = "synthetic seeded (seed 1234), fan-in scaled"
             self.encoder = a.encoder
-        self.x = torch.from_numpy(self.images(self.B, rank * self.B)).cuda()
-        self.y = {k: torch.empty(v, device="cuda") for k, v in self.outs.items()}
+        if B > 0:
+            self.x = torch.from_numpy(self.images(B, first)).cuda()
+            self.y = {k: torch.empty(v, device="cuda") for k, v in self.outs.items()}
 
     def b1_legs(self, a, dev):
         res = b1_reference_method(self.blob, dev, self.images(1, 0), a.b1_warmup, a.b1_iters, self.ref_fps)
@@ -357,15 +325,42 @@ class Workload:
         return res
 
 
+DEFAULT_BATCH = {"depth_pro": 4, "vggt": 8,
+                 # B=28: attention runs 256-query workgroups (6 per head at T=1370),
+                 # 2 per CU -> 28 x 6 heads x 6 = 1008 workgroups = two full rounds
+                 # of 512 (B=30: 1080, a third round 11 % full: 122 vs 103 us per
+                 # launch, the same 4290 img/s overall); the N=384 GEMMs' 128^2
+                 # tiles also stay within whole rounds (B=32: 1029 for 1024 slots,
+                 # profiles/r01_v18_batch_sweep.json)
+                 "depth_anything_v2": 28}
+
+
+def rank_work(a, world, rank):
+    """(items on this rank, first item seed, items per step over all ranks,
+    scaling, description) -- weak: --batch per GPU; strong: --global-batch
+    sharded contiguously (replicas.shard), an idle rank possible."""
+    from monocular_depth_estimation_trt_amd import replicas
+    if a.global_batch > 0:
+        first, B = replicas.shard(a.global_batch, world, rank)
+        return B, first, a.global_batch, "strong", f"global batch {a.global_batch} sharded over {world} GPU(s)"
+    B = a.batch or DEFAULT_BATCH[a.model]
+    return B, rank * B, world * B, "weak", f"batch {B} per GPU"
+
+
 def main():
     a = parse()
-    import torch
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if "WORLD_SIZE" not in os.environ and a.gpus > 1:
+        # self-launch: one child process per GPU, started before this process
+        # touches the GPU (it never does); rank 0's JSON line is the output
+        from monocular_depth_estimation_trt_amd import replicas
+        raise SystemExit(replicas.spawn_local(a.gpus, os.path.abspath(__file__), sys.argv[1:]))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}: launch one process per GPU")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != a.gpus:
-        if world == 1 and a.gpus > 1:
-            raise SystemExit("--gpus N > 1 must be launched with torch.distributed.run (one process per GPU)")
+
+    import torch
     dist = None
     if world > 1:
         import torch.distributed as dist
@@ -373,63 +368,79 @@ def main():
         dist.init_process_group("gloo", rank=rank, world_size=world)
     torch.cuda.set_device(local)
 
+    from monocular_depth_estimation_trt_amd import replicas
     from monocular_depth_estimation_trt_amd.engine import Engine
 
-    wl = Workload(a, rank)
-    B, S = wl.B, wl.S
-    shape = tuple(wl.x.shape)
-    eng = Engine.from_bytes(wl.blob, local, profile=((1,) + shape[1:], shape, shape))
-    ctx = eng.create_execution_context()
-    ctx.set_input_shape(wl.input_name, shape)
-    ctx.set_tensor_address(wl.input_name, wl.x.data_ptr())
-    for k, t in wl.y.items():
-        ctx.set_tensor_address(k, t.data_ptr())
+    B, first, total_items, scaling, a.per_gpu_desc = rank_work(a, world, rank)
+    wl = Workload(a, B, first)
+    S = wl.S
+    ctx = eng = None
+    if B > 0:
+        shape = tuple(wl.x.shape)
+        eng = Engine.from_bytes(wl.blob, local, profile=((1,) + shape[1:], shape, shape))
+        ctx = eng.create_execution_context()
+        ctx.set_input_shape(wl.input_name, shape)
+        ctx.set_tensor_address(wl.input_name, wl.x.data_ptr())
+        for k, t in wl.y.items():
+            ctx.set_tensor_address(k, t.data_ptr())
     st = torch.cuda.Stream()
     sh = st.cuda_stream
+    step = (lambda: ctx.execute_async_v3(sh)) if ctx is not None else (lambda: None)
 
-    from monocular_depth_estimation_trt_amd import replicas
     for _ in range(a.warmup):
-        ctx.execute_async_v3(sh)
+        step()
     torch.cuda.synchronize()
-    el = replicas.timed_region(lambda: ctx.execute_async_v3(sh), a.steps, torch.cuda.synchronize,
+    el = replicas.timed_region(step, a.steps, torch.cuda.synchronize,
                                dist.barrier if dist is not None else None)
+    per_rank = replicas.gather_to_rank0(round(el, 6))
     el = replicas.max_over_ranks(el)
-    out_ok = all(bool(torch.isfinite(t).all().item()) for t in wl.y.values())
-    value = world * B * wl.frames * a.steps / el
+    out_ok = all(bool(torch.isfinite(t).all().item()) for t in wl.y.values()) if B > 0 else True
+    value = total_items * wl.frames * a.steps / el
     ms_step = el / a.steps * 1e3
 
     if rank != 0:
+        if ctx is not None:
+            ctx.destroy()
+            eng.destroy()
         if dist is not None:
             dist.barrier()
             dist.destroy_process_group()
         return
 
     layer_ms = profile_layers(ctx, sh, a.profile_iters)
-    roof, breakdown = roofline(wl.cfg, B, S, layer_ms, wl.frames)
+    tfile = traffic_path(a.model, wl.encoder, B, S, wl.frames)
+    roof, breakdown = roofline(wl.cfg, B, S, layer_ms, wl.frames, tfile)
     if a.layers_json:
         with open(a.layers_json, "w") as f:
             json.dump({"batch": B, "frames": wl.frames, "layer_ms": layer_ms, "classes": breakdown, "roofline": roof},
                       f, indent=1)
+    # MFMA fraction of the whole job: every GPU's share of the work at the job's rate
     model_frac = value / world * wl.gflop * 1e9 / (MFMA_PEAK_TFLOPS * 1e12)
     ctx.destroy()
     eng.destroy()
     res_b1 = {} if a.no_b1 else wl.b1_legs(a, local)
+    if "b1_compute_ms" in res_b1:
+        # batch-1 forward (the engine compute of one image, hipEvent-timed inside do_inference)
+        res_b1["b1_model_mfma_frac"] = round(wl.gflop * 1e9 / (res_b1["b1_compute_ms"] * 1e-3) /
+                                             (MFMA_PEAK_TFLOPS * 1e12), 4)
     cpu = None
     if world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(wl.cfg, S, a.cpu_seconds)
     for c, v in list(breakdown.items())[:10]:
         log(f"{c:24s} {v['ms']:9.4f} ms  x{v['launches']:3d}  {v['tflops']} TF/s")
     config = {"workload": wl.workload, "encoder": wl.encoder, "img": [S, S], "batch_per_gpu": B,
-              "global_batch": B * world, "parallelism": f"replica x{world} (batch shards, no collectives)",
+              "global_batch": total_items, "parallelism": f"replica x{world} (batch shards, no collectives)",
               "weights": wl.weights}
     if a.model == "vggt":
         config["frames"] = wl.frames
     line = {
         "metric": f"depth FPS (images/s) at {S}x{S} fp16, {wl.label}, MI355X",
         "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
-        "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": round(value / wl.ref_fps, 3), "dtype": "fp16", "data": "synthetic",
+        "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": scaling,
+        "vs_baseline": None, "throughput_vs_ref_b1": round(value / wl.ref_fps, 3),
+        "dtype": "fp16", "data": "synthetic",
         "config": config,
+        "rank_seconds": per_rank,
         "model_gflop_per_image": round(wl.gflop, 2),
         "model_mfma_frac": round(model_frac, 4),
         "roofline": roof,

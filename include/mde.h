@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MDE_ABI_VERSION 4
+#define MDE_ABI_VERSION 5
 
 typedef enum {
   MDE_OK = 0,
@@ -154,10 +154,15 @@ int mde_op_qkv(const void* a_f16, const void* w_f16, int ldw, const float* bias,
                int heads, int tokens_pad, float q_scale, void* q_f16, void* k_f16, void* vt_f16, void* stream);
 /* q pre-multiplied by dh^-0.5 * log2(e) (scores in log2 units, as mde_op_qkv writes with
  * q_scale = 0.125 * log2(e)); k/q [B*H][tokens_pad][64], vt [B*H][64][tokens_pad] with key t
- * stored at column vt_pos(t) = (t & ~31) | ((t & 15) >> 2) << 3 | ((t & 31) >> 4) << 2 | (t & 3)
- * (the layout mde_op_qkv writes). */
+ * stored at column vt_pos(t) = t with bits 2 and 3 swapped, (t & ~12) | (t & 4) << 1 | (t & 8) >> 1
+ * (the layout mde_op_qkv writes); ldo % 8 == 0 and o 16-B aligned. */
 int mde_op_attention(const void* q_f16, const void* k_f16, const void* vt_f16, void* o_f16, int batch, int heads,
                      int tokens, int tokens_pad, int ldo, void* stream);
+/* The same with an fp32 workspace for the split-KV path the launcher takes when the (head, query
+ * block) grid is too small to fill the chip (batch 1); mde_op_attention_ws_bytes gives its size. */
+int mde_op_attention_ws(const void* q_f16, const void* k_f16, const void* vt_f16, void* o_f16, int batch, int heads,
+                        int tokens, int tokens_pad, int ldo, void* ws, size_t ws_bytes, void* stream);
+size_t mde_op_attention_ws_bytes(int batch, int heads, int tokens);
 int mde_op_patch_embed(const float* img, int batch, int h, int w, const void* w_f16, int ldw, const float* bias,
                        const float* pos_patch, const float* cls_pos, int dim, void* patch_scratch_f16,
                        float* x32, void* stream);
@@ -212,13 +217,6 @@ int mde_op_qk_norm_rope(void* q_f16, void* k_f16, const float* q_gamma, const fl
  * (xa, xb fp32 [nseq][tokens][dim]) -> f16 [nseq * (tokens - npre)][2*dim]. */
 int mde_op_tap_concat_ln(const float* xa, const float* xb, int nseq, int tokens, int npre, int dim,
                          const float* gamma, const float* beta, float eps, void* out_f16, void* stream);
-/* Fused ViT-S MLP + LayerScale residual (upstream DINOv2 Block ffn):
- * x32[m] += ls2 * (GELU(a[m] . w1^T + b1) . w2^T + b2), the hidden activation rounded to f16 as
- * the unfused fc1 stores it; a f16 [m][dim], w1 [hidden][ldw1], w2 [dim][ldw2]; supported:
- * dim 384, hidden 1536, ldw1 384, ldw2 1536 (else MDE_ERR_ARG). */
-int mde_op_mlp_residual(const void* a_f16, int m, const void* w1_f16, int ldw1, const float* b1, const void* w2_f16,
-                        int ldw2, const float* b2, const float* ls2, float* x32, int dim, int hidden, void* stream);
-
 #ifdef __cplusplus
 }
 #endif

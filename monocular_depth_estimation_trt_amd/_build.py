@@ -20,8 +20,8 @@ INCLUDE = os.path.join(ROOT, "include")
 LIB = os.path.join(HERE, "libmde_hip.so")
 OBJDIR = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("MDE_OFFLOAD_ARCH", "gfx950")
-SOURCES = ["gemm.hip", "gemm_persistent.hip", "conv.hip", "attention.hip", "elementwise.hip", "engine.hip",
-           "depth_pro.hip", "depth_pro_ops.hip", "gemm256.hip", "vggt.hip", "vggt_ops.hip", "mlp_fused.hip"]
+SOURCES = ["gemm.hip", "conv.hip", "attention.hip", "elementwise.hip", "engine.hip",
+           "depth_pro.hip", "depth_pro_ops.hip", "gemm256.hip", "vggt.hip", "vggt_ops.hip"]
 # attention: no NaN inputs by construction (masked keys are -inf, never NaN);
 # lets fmaxf lower to a bare v_max_f32 without canonicalising moves
 PER_FILE = {"attention.hip": ["-fno-honor-nans"]}
@@ -62,8 +62,14 @@ def up_to_date() -> bool:
 
 def build_library(force: bool = False, verbose: bool = True, out: str = "", defines=()) -> str:
     """Build the library; `out`/`defines` build a tuning variant elsewhere
-    (e.g. defines=("MDE_GEMM_BK=32",)) without touching the product .so."""
+    (e.g. defines=("MDE_GEMM_BK=32",)) without touching the product .so: a
+    variant with defines but no `out` goes to build/var/lib_<hash>.so."""
     variant = bool(out or defines)
+    if defines and not out:
+        out = os.path.join(ROOT, "build", "var", "lib_" + hashlib.sha1("|".join(defines).encode()).hexdigest()[:10] + ".so")
+        os.makedirs(os.path.dirname(out), exist_ok=True)
+    if variant and os.path.abspath(out) == os.path.abspath(LIB):
+        raise ValueError("a tuning variant must not overwrite the product libmde_hip.so")
     if not variant and not force and up_to_date():
         return LIB
     cc = hipcc()

@@ -89,6 +89,9 @@ PROTOTYPES = {
                                c_void_p, c_int, c_void_p],
     "mde_op_qkv": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p,
                    c_void_p, c_void_p],
+    "mde_op_attention_ws": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
+                            c_size_t, c_void_p],
+    "mde_op_attention_ws_bytes": [c_int, c_int, c_int],
     "mde_op_attention": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "mde_op_patch_embed": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                            c_void_p, c_void_p, c_void_p],
@@ -110,10 +113,8 @@ PROTOTYPES = {
     "mde_op_qk_norm_rope": [c_void_p] * 6 + [c_int] * 6 + [c_void_p, c_void_p, c_float, c_float, c_void_p],
     "mde_op_tap_concat_ln": [c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p, c_float, c_void_p,
                              c_void_p],
-    "mde_op_mlp_residual": [c_void_p, c_int, c_void_p, c_int, c_void_p, c_void_p, c_int, c_void_p, c_void_p,
-                            c_void_p, c_int, c_int, c_void_p],
 }
-_RESTYPE = {"mde_last_error": c_char_p}
+_RESTYPE = {"mde_last_error": c_char_p, "mde_op_attention_ws_bytes": c_size_t}
 
 _lib = None
 _lock = threading.Lock()

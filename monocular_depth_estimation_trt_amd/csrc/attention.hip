@@ -5,24 +5,40 @@
 // Layouts (written by the qkv GEMM epilogue, E_QKV):
 //   q, k : [B*H][Tpad][64] f16, q pre-multiplied by dh^-0.5 * log2(e), so the
 //          scores come out in log2 units and exp() is one v_exp_f32 (exp2)
-//   vt   : [B*H][64][Tpad] f16 (v transposed; key t stored at vt_pos(t), a
-//          permutation inside each 32-key group), pad columns t >= T zero
+//   vt   : [B*H][64][Tpad] f16 (v transposed; key t stored at vt_pos(t) = t
+//          with bits 2 and 3 swapped, see below), pad columns t >= T zero
 //   o    : [B*T][ldo] f16, head h in columns h*64 .. h*64+63
 //
-// Structure.  A workgroup = NW waves; a wave owns QW (16 or 32) queries as
-// 16-query column blocks.  The score tile is computed TRANSPOSED, S^T = K Q^T,
-// so the query sits on the MFMA lane: the online-softmax max / sum over keys
-// is a reduction over the lane's registers plus two lane shuffles (xor 16,
-// 32), and P^T feeds the P.V MFMA as the B operand straight from the
-// accumulators (O^T = V^T P^T), no LDS round trip.  K and V^T key tiles (64
-// keys) stream global -> LDS by global_load_lds through a 3-slot ring, two
-// tiles in flight, counted `s_waitcnt vmcnt` + raw s_barrier (a
-// __syncthreads() would drain the DMA).  LDS images are lane-linear with the
-// swizzle chunk ^ (row & 7) applied on the source address (conflict-free
-// ds_read_b128 for both).  The running max rides in the score MFMA's C
-// operand (S' = QK^T - m), so the softmax is max-check + exp2 + sum per
-// element; O and l are rescaled only when a max grows.  Softmax statistics in
-// fp32; keys >= T are masked on the last tile only.
+// Structure.  A workgroup = NW waves, a wave owns 32 queries, and both
+// products run on v_mfma_f32_32x32x16_f16: every K / V^T fragment read from
+// LDS feeds 32 queries.  The score tile is computed TRANSPOSED, S^T = K Q^T
+// (A = K, 32 keys x 16 dims; B = Q^T), so the query sits on the lane: a lane
+// holds 16 keys of one query per 32-key block, lanes l and l+32 the other 16
+// -- the row max / sum is a register reduction plus ONE v_permlane32_swap.
+// S^T's accumulator is directly the B operand of O^T = V^T P^T: registers
+// 8s..8s+7 of a key block are k-step s, whose element j of lane half h is key
+// 16s + 8(j>>2) + 4h + (j&3); V^T stores key t at vt_pos(t) (bits 2,3 of t
+// swapped) so those 8 keys are one contiguous 16-B read.  K and V^T tiles (64
+// keys) stream global -> LDS by global_load_lds through a 2-slot ring (tile
+// kt+1 in flight while kt is computed), counted `s_waitcnt vmcnt` + raw
+// s_barrier; LDS rows are 128 B with chunk swizzle c ^ ((row >> 1) & 7)
+// applied on the source address (conflict-free ds_read_b128 for the 32-row x
+// 2-chunk operand reads; SQ_LDS_BANK_CONFLICT = 0 measured).  A 64-key tile
+// is two 32-key blocks, each run start to finish (scores, softmax, P.V) so
+// one 16-register score accumulator is live.  The running max rides in the
+// score MFMA's C operand (S' = QK^T - m), O and l are rescaled only when a
+// max grows past a threshold (deferred rescale).  Softmax statistics in fp32;
+// keys >= T masked on the last block only.  The epilogue pairs lane halves
+// with v_permlane32_swap so each lane stores 16 B of one output row.
+//
+// Small grids (batch 1: 6 or 16 heads x a few query blocks) split the key
+// range over gridDim.z: each split writes its unnormalised fp32 O with its
+// running max and sum, and attn_combine_kernel merges them.
+//
+// Measured alternatives (MI355X, B = 28): two 32-query
+// sub-blocks per wave (256 VGPRs), 128-key tiles, a 3-slot ring, one-block
+// software pipelining and an 8-wave ping-pong of MFMA / softmax segments were
+// all slower than this form (110 us; the 16x16x32 predecessor ~120 us).
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
@@ -34,34 +50,39 @@ namespace mde {
 
 namespace {
 
-constexpr int KT = 64;        // keys per tile
+constexpr int KT = 64;            // keys per tile (and Tpad granularity)
 constexpr int TILE_B = KT * 128;  // bytes of one K (or V^T) tile image: 64 rows x 128 B
+constexpr int SLOT = 2 * TILE_B;  // K + V^T
+constexpr int QW = 32;            // queries per wave (one 32-column MFMA block)
 
-typedef f16 f16x4v __attribute__((ext_vector_type(4)));
-typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+MDE_DEV f32x16 mfma32(const f16x8& a, const f16x8& b, const f32x16& c) {
+  // D[32x32] += A[32x16] B[16x32]; lane l: A[l&31][8(l>>5)+j], B[8(l>>5)+j][l&31];
+  // D col l&31, row (r&3) + 8(r>>2) + 4(l>>5) for register r
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
 
 // Deferred rescale (cdna_hip_programming.md 5.5 T13): the running max moves
-// only when a tile's max exceeds it by more than RESCALE_T (log2 units), so
+// only when a block's max exceeds it by more than RESCALE_T (log2 units), so
 // p = exp2(S - m_run) <= 2^RESCALE_T = 256 -- exact in f16's range, and the
-// rescale branch (O, l *= 2^-delta) is taken a few times per row, not per tile.
+// rescale branch (O, l *= 2^-delta) is taken a few times per row, not per block.
 constexpr float RESCALE_T = 8.f;
 
-// byte offset of 16-B chunk `chunk` of a 128-B row: conflict-free ds_read_b128
-MDE_DEV int kswz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+// byte offset of 16-B chunk `chunk` of a 128-B row.  The 32x32x16 operand
+// read takes rows r0..r0+31 (lanes 0-31) at chunk c and the same rows at
+// chunk c+1 (lanes 32-63); a ds_read_b128 lane group covers rows of both
+// parities, and (row >> 1) & 7 spreads each parity's 8 rows over 8 chunks:
+// every 16-lane group touches 64 distinct banks
+MDE_DEV int swz(int row, int chunk) { return row * 128 + ((chunk ^ ((row >> 1) & 7)) << 4); }
 
-// max / sum over the 4 lanes {l, l^16, l^32, l^48} with VALU lane swaps
-// (v_permlane16/32_swap) instead of LDS-routed shuffles
-MDE_DEV float xmax4(float x) {
-  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  x = fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
-  auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return fmaxf(__uint_as_float(r2[0]), __uint_as_float(r2[1]));
+MDE_DEV float swap_max(float x) {  // max over lanes l and l ^ 32
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
-MDE_DEV float xsum4(float x) {
-  auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  x = __uint_as_float(r[0]) + __uint_as_float(r[1]);
-  auto r2 = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return __uint_as_float(r2[0]) + __uint_as_float(r2[1]);
+MDE_DEV float swap_sum(float x) {
+  auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
 }
 
 template <int N>
@@ -77,17 +98,29 @@ MDE_DEV void lds_barrier() {
   asm volatile("" ::: "memory");
 }
 
-template <int QW, int NW>
-__global__ void __launch_bounds__(NW * 64) attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k,
-                                                           const f16* __restrict__ vt, f16* __restrict__ o, int H,
-                                                           int T, int Tpad, int ldo) {
-  constexpr int NQ = QW / 16;            // 16-query blocks per wave
-  constexpr int BQ = QW * NW;            // queries per workgroup
-  constexpr int INS = 8 / NW;            // glds instructions per wave per image (8 per 64-row image)
-  constexpr int PER_TILE = 2 * INS;      // K + V^T
-  constexpr int SLOT = 2 * TILE_B;
-  static_assert(8 % NW == 0, "waves must divide the 8 glds instructions of a tile");
-  __shared__ __attribute__((aligned(16))) char smem[3 * SLOT];
+MDE_DEV unsigned pack2(float a, float b) {
+  typedef f16 f16x2 __attribute__((ext_vector_type(2)));
+  const f16x2 h = {(f16)a, (f16)b};
+  return __builtin_bit_cast(unsigned, h);
+}
+
+// Split-KV partials: per (split, sequence*head, padded query) the
+// unnormalised O row (fp32 x 64) and (m, l) in log2 units.
+struct SplitWs {
+  float* o = nullptr;   // [S][BH][Tq][64]
+  float* ml = nullptr;  // [S][BH][Tq][2]
+  int Tq = 0;           // padded queries per (b, h): gridDim.x * BQ
+  int tiles = 0;        // key tiles per split
+};
+
+template <int NW, bool SPLIT>
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4, 8)))
+attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16* __restrict__ vt,
+                f16* __restrict__ o, int H, int T, int Tpad, int ldo, SplitWs ws) {
+  constexpr int BQ = QW * NW;    // queries per workgroup
+  constexpr int INS = 8 / NW;    // glds instructions per wave per image (8 per 64-row image)
+  static_assert(NW == 4 || NW == 8, "waves per workgroup");
+  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -104,21 +137,25 @@ __global__ void __launch_bounds__(NW * 64) attn_fwd_kernel(const f16* __restrict
   const int bh = lin / nqb;
   const int b = bh / H, h = bh - (bh / H) * H;
   const int qbase = (lin - bh * nqb) * BQ + wave * QW;
-  const int l15 = lane & 15, hq = lane >> 4;
+  const bool active = qbase < T;  // wave-uniform: a wave past the last query only helps load
+  const int l31 = lane & 31, hh = lane >> 5;
+
+  // key tiles [kt0, kt1) of this workgroup (all of them unless split)
+  const int nkt_all = (T + KT - 1) / KT;
+  const int kt0 = SPLIT ? (int)blockIdx.z * ws.tiles : 0;
+  const int kt1 = SPLIT ? min(nkt_all, kt0 + ws.tiles) : nkt_all;
 
   const f16* qb = q + (size_t)bh * Tpad * 64;
   const f16* kb = k + (size_t)bh * Tpad * 64;
   const f16* vb = vt + (size_t)bh * 64 * Tpad;
 
-  // Q^T fragments (B operand): lane holds Q[q][32s + 8hq + j] of its query column
-  f16x8 qf[NQ][2];
+  // Q^T fragments (B operand), k-step s = dims 16s..16s+15: lane holds
+  // Q[query][16s + 8hh + j] of its query column
+  const int qi = qbase + l31;
+  f16x8 qf[4];
 #pragma unroll
-  for (int c = 0; c < NQ; ++c)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int qi = qbase + c * 16 + l15;
-      qf[c][s] = qi < Tpad ? *reinterpret_cast<const f16x8*>(qb + (size_t)qi * 64 + 32 * s + 8 * hq) : zero8();
-    }
+  for (int st = 0; st < 4; ++st)
+    qf[st] = qi < Tpad ? *reinterpret_cast<const f16x8*>(qb + (size_t)qi * 64 + 16 * st + 8 * hh) : zero8();
 
   // glds geometry: lane -> row lrow of an 8-row group, physical chunk lane & 7
   const int lrow = lane >> 3, pc = lane & 7;
@@ -129,209 +166,270 @@ __global__ void __launch_bounds__(NW * 64) attn_fwd_kernel(const f16* __restrict
     for (int i = 0; i < INS; ++i) {
       const int g = wave * INS + i;  // 8-row group 0..7
       const int row = g * 8 + lrow;
-      const int kch = pc ^ (row & 7);
-      __builtin_amdgcn_global_load_lds(kb + (size_t)(kt * KT + row) * 64 + kch * 8, sK + g * 8 * 128, 16, 0, 0);
-      __builtin_amdgcn_global_load_lds(vb + (size_t)row * Tpad + kt * KT + kch * 8, sV + g * 8 * 128, 16, 0, 0);
+      const int lc = pc ^ ((row >> 1) & 7);
+      __builtin_amdgcn_global_load_lds(kb + (size_t)(kt * KT + row) * 64 + lc * 8, sK + g * 8 * 128, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(vb + (size_t)row * Tpad + kt * KT + lc * 8, sV + g * 8 * 128, 16, 0, 0);
     }
   };
 
-  // running max per query (log2 units) as an MFMA C operand: every tile after
-  // the first computes S' = S - m_run directly in the accumulator, so
-  // p = exp2(S') needs no subtraction unless some max grew (rare branch)
-  float m_run[NQ], l_run[NQ];
-  f32x4 negm[NQ];
-  f32x4 acc[NQ][4];
+  // running max (log2 units) as an MFMA C operand: after the first block the
+  // score MFMA computes S' = S - m_run directly in the accumulator
+  float m_run = 0.f, l_run = 0.f;
+  f32x16 negm, acc[2];
 #pragma unroll
-  for (int c = 0; c < NQ; ++c) {
-    m_run[c] = 0.f;
-    l_run[c] = 0.f;
-    negm[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int d = 0; d < 4; ++d) acc[c][d] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int r = 0; r < 16; ++r) {
+    negm[r] = 0.f;
+    acc[0][r] = 0.f;
+    acc[1][r] = 0.f;
   }
 
-  const int nkt = (T + KT - 1) / KT;
-  issue(0, 0);
-  if (nkt > 1) {
-    issue(1, 1);
-    wait_vm_n<PER_TILE>();
-  } else {
-    wait_vm_n<0>();
-  }
+  issue(kt0, 0);
+  wait_vm_n<0>();
   lds_barrier();
 
   auto tile = [&](int kt, auto slot_tag, auto first_tag) {
-    constexpr bool FIRST = decltype(first_tag)::value;
+    constexpr bool FIRST_TILE = decltype(first_tag)::value;
     constexpr int slot = decltype(slot_tag)::value;  // compile-time: LDS offsets fold into ds_read immediates
     const char* K_ = smem + slot * SLOT;
     const char* V_ = K_ + TILE_B;
-    // S'^T[key][query] = K Q^T - m_run: 4 key sub-tiles x NQ query blocks
-    f32x4 s[NQ][4];
 #pragma unroll
-    for (int t4 = 0; t4 < 4; ++t4) {
-      const int row = t4 * 16 + l15;
-      const f16x8 k0 = *reinterpret_cast<const f16x8*>(K_ + kswz(row, hq));
-      const f16x8 k1 = *reinterpret_cast<const f16x8*>(K_ + kswz(row, 4 + hq));
+    for (int kb2 = 0; kb2 < 2; ++kb2) {
+      const bool FIRST = FIRST_TILE && kb2 == 0;  // compile-time after unrolling
+      // S'^T[key][query] = K Q^T - m_run over 32 keys: 4 dim k-steps
+      f32x16 sc;
+      if (FIRST) {
 #pragma unroll
-      for (int c = 0; c < NQ; ++c) {
-        s[c][t4] = mfma16x16x32(k0, qf[c][0], FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : negm[c]);
-        s[c][t4] = mfma16x16x32(k1, qf[c][1], s[c][t4]);
+        for (int r = 0; r < 16; ++r) sc[r] = 0.f;
+      } else {
+        sc = negm;
       }
-    }
-    if (kt * KT + KT > T) {  // last, partial tile: keys >= T -> -inf
-      const int key0 = kt * KT + hq * 4;
+      const int krow = kb2 * 32 + l31;
 #pragma unroll
-      for (int c = 0; c < NQ; ++c)
+      for (int st = 0; st < 4; ++st) {
+        const f16x8 kf = *reinterpret_cast<const f16x8*>(K_ + swz(krow, 2 * st + hh));
+        sc = mfma32(kf, qf[st], sc);
+      }
+      if (kt * KT + kb2 * 32 + 32 > T) {  // last, partial block: keys >= T -> -inf
+        const int key0 = kt * KT + kb2 * 32 + 4 * hh;
 #pragma unroll
-        for (int t4 = 0; t4 < 4; ++t4)
+        for (int r = 0; r < 16; ++r)
+          if (key0 + (r & 3) + 8 * (r >> 2) >= T) sc[r] = -INFINITY;
+      }
+      // max over the lane's 16 scores (v_max3 chain) and its partner lane
+      float mx = fmaxf(sc[0], sc[1]);
 #pragma unroll
-          for (int r = 0; r < 4; ++r)
-            if (key0 + t4 * 16 + r >= T) s[c][t4][r] = -INFINITY;
-    }
-    f16x8 pb[NQ][2];
-#pragma unroll
-    for (int c = 0; c < NQ; ++c) {
-      // max over the lane's 16 scores as a chain of v_max3 (8 ops)
-      float mx = fmaxf(fmaxf(s[c][0][0], s[c][0][1]), s[c][0][2]);
-      mx = fmaxf(fmaxf(mx, s[c][0][3]), s[c][1][0]);
-      mx = fmaxf(fmaxf(mx, s[c][1][1]), s[c][1][2]);
-      mx = fmaxf(fmaxf(mx, s[c][1][3]), s[c][2][0]);
-      mx = fmaxf(fmaxf(mx, s[c][2][1]), s[c][2][2]);
-      mx = fmaxf(fmaxf(mx, s[c][2][3]), s[c][3][0]);
-      mx = fmaxf(fmaxf(mx, s[c][3][1]), s[c][3][2]);
-      mx = fmaxf(mx, s[c][3][3]);
-      mx = xmax4(mx);  // max of S' over the tile (relative to m_run)
+      for (int r = 2; r < 16; r += 2) mx = fmaxf(fmaxf(mx, sc[r]), sc[r + 1]);
+      mx = swap_max(mx);  // max of S' over the block (relative to m_run)
       if (FIRST || __any(mx > RESCALE_T)) {
         // the running max grows by delta >= 0: shift S', rescale O and l
         const float delta = FIRST ? mx : fmaxf(mx, 0.f);
-        m_run[c] += delta;
-        negm[c] = f32x4{-m_run[c], -m_run[c], -m_run[c], -m_run[c]};
+        m_run += delta;
 #pragma unroll
-        for (int t4 = 0; t4 < 4; ++t4) s[c][t4] -= delta;
+        for (int r = 0; r < 16; ++r) negm[r] = -m_run;
+        sc -= delta;
         if (!FIRST) {
           const float alpha = __builtin_amdgcn_exp2f(-delta);
-          l_run[c] *= alpha;
-#pragma unroll
-          for (int d = 0; d < 4; ++d) acc[c][d] *= alpha;
+          l_run *= alpha;
+          acc[0] *= alpha;
+          acc[1] *= alpha;
         }
       }
-      f32x2 ls2 = {0.f, 0.f};  // packed row sums (v_pk_add_f32)
+      // P = exp2(S'), row sums, and P^T as the PV B operand: registers
+      // 8s..8s+7 are k-step s (keys 16s + 8(j>>2) + 4hh + (j&3))
+      f16x8 pb[2];
+      float ls0 = 0.f, ls1 = 0.f;
 #pragma unroll
-      for (int t4 = 0; t4 < 4; ++t4)
+      for (int r = 0; r < 16; r += 2) {
+        const float p0 = __builtin_amdgcn_exp2f(sc[r]), p1 = __builtin_amdgcn_exp2f(sc[r + 1]);
+        ls0 += p0;
+        ls1 += p1;
+        pb[r >> 3][r & 7] = (f16)p0;
+        pb[r >> 3][(r & 7) + 1] = (f16)p1;
+      }
+      l_run += ls0 + ls1;
+      // O^T[dh][q] += V^T[dh][key] P^T[key][q]: two 32-row dh blocks x 2 key k-steps
 #pragma unroll
-        for (int r = 0; r < 4; r += 2) {
-          const f32x2 pv = {__builtin_amdgcn_exp2f(s[c][t4][r]), __builtin_amdgcn_exp2f(s[c][t4][r + 1])};
-          s[c][t4][r] = pv[0];
-          s[c][t4][r + 1] = pv[1];
-          ls2 += pv;
+      for (int db = 0; db < 2; ++db) {
+        const int vrow = db * 32 + l31;
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          const f16x8 vf = *reinterpret_cast<const f16x8*>(V_ + swz(vrow, 2 * (2 * kb2 + g) + hh));
+          acc[db] = mfma32(vf, pb[g], acc[db]);
         }
-      l_run[c] += ls2[0] + ls2[1];
-      // P^T as B operand: k index j<4 -> key sub-tile 2ks, j>=4 -> 2ks+1 (rows 4hq+r)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          pb[c][ks][r] = (f16)s[c][2 * ks][r];
-          pb[c][ks][4 + r] = (f16)s[c][2 * ks + 1][r];
-        }
-    }
-    // O^T[dh][q] += V^T[dh][key] P^T[key][q]; V^T keys are stored vt_pos-
-    // permuted, so the 8 keys of k-step ks for lane slot hq are one 16-B chunk
-#pragma unroll
-    for (int d = 0; d < 4; ++d) {
-      const int row = d * 16 + l15;
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const f16x8 af = *reinterpret_cast<const f16x8*>(V_ + kswz(row, 4 * ks + hq));
-#pragma unroll
-        for (int c = 0; c < NQ; ++c) acc[c][d] = mfma16x16x32(af, pb[c][ks], acc[c][d]);
       }
     }
   };
 
-  // tile kt lives in ring slot kt % 3; the loop is unrolled over the three
-  // slots so every LDS address is lane base + immediate
+  // tile kt lives in ring slot (kt - kt0) & 1; the loop is unrolled over the
+  // two slots so every LDS address is lane base + immediate.  Tile kt+1 is
+  // issued into the other slot (released by the previous barrier) before
+  // tile kt is computed, and must land before the barrier that ends the step.
   auto step = [&](int kt, auto slot_tag, auto first_tag) {
     constexpr int SL = decltype(slot_tag)::value;
-    if (kt + 2 < nkt) issue(kt + 2, (SL + 2) % 3);
-    tile(kt, slot_tag, first_tag);
-    // tile kt+1 must have landed before anyone reads it; its slot's previous
-    // contents (tile kt-2) were released at the previous barrier
-    if (kt + 2 < nkt) wait_vm_n<PER_TILE>();
-    else wait_vm_n<0>();
+    if (kt + 1 < kt1) issue(kt + 1, SL ^ 1);
+    if (active) tile(kt, slot_tag, first_tag);
+    wait_vm_n<0>();
     lds_barrier();
   };
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
-  using S2 = std::integral_constant<int, 2>;
-  step(0, S0{}, std::true_type{});
-  int kt = 1;
-  for (; kt + 3 <= nkt; kt += 3) {
+  step(kt0, S0{}, std::true_type{});
+  int kt = kt0 + 1;
+  for (; kt + 2 <= kt1; kt += 2) {
     step(kt, S1{}, std::false_type{});
-    step(kt + 1, S2{}, std::false_type{});
-    step(kt + 2, S0{}, std::false_type{});
+    step(kt + 1, S0{}, std::false_type{});
   }
-  if (kt < nkt) step(kt++, S1{}, std::false_type{});
-  if (kt < nkt) step(kt++, S2{}, std::false_type{});
+  if (kt < kt1) step(kt, S1{}, std::false_type{});
+  if (!active) return;
 
+  if constexpr (SPLIT) {
+    // unnormalised O^T (relative to m_run) and (m, l) of this key range
+    const float lt = swap_sum(l_run);
+    const size_t row = ((size_t)blockIdx.z * gridDim.y + bh) * ws.Tq + qi;
+    float* orow = ws.o + row * 64;
 #pragma unroll
-  for (int c = 0; c < NQ; ++c) {
-    const float lt = xsum4(l_run[c]);
-    const float inv = 1.f / lt;
-    const int qi = qbase + c * 16 + l15;
-    if (qi < T) {
-      f16* orow = o + ((size_t)b * T + qi) * ldo + h * 64;
+    for (int db = 0; db < 2; ++db)
 #pragma unroll
-      for (int d = 0; d < 4; ++d) {
-        f16x4v v;
+      for (int g4 = 0; g4 < 4; ++g4)
+        *reinterpret_cast<float4*>(orow + 32 * db + 8 * g4 + 4 * hh) =
+            make_float4(acc[db][4 * g4], acc[db][4 * g4 + 1], acc[db][4 * g4 + 2], acc[db][4 * g4 + 3]);
+    if (hh == 0) *reinterpret_cast<float2*>(ws.ml + row * 2) = make_float2(m_run, lt);
+    return;
+  }
+
+  // epilogue: lane holds O^T[dh = 32 db + (r&3) + 8(r>>2) + 4hh][qi]; pair
+  // register groups (r>>2) = 2pr, 2pr+1 across the lane halves
+  // (v_permlane32_swap) so each lane stores dh 16pr + 8hh .. +7 as one 16-B write
+  const float inv = 1.f / swap_sum(l_run);
+  uint4 out[2][2];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = (f16)(acc[c][d][r] * inv);
-        *reinterpret_cast<f16x4v*>(orow + d * 16 + hq * 4) = v;
-      }
+  for (int db = 0; db < 2; ++db)
+#pragma unroll
+    for (int pr = 0; pr < 2; ++pr) {
+      const int r0 = 8 * pr;  // group 2pr: registers r0..r0+3, group 2pr+1: r0+4..r0+7
+      const unsigned ax = pack2(acc[db][r0] * inv, acc[db][r0 + 1] * inv);
+      const unsigned ay = pack2(acc[db][r0 + 2] * inv, acc[db][r0 + 3] * inv);
+      const unsigned bx = pack2(acc[db][r0 + 4] * inv, acc[db][r0 + 5] * inv);
+      const unsigned by = pack2(acc[db][r0 + 6] * inv, acc[db][r0 + 7] * inv);
+      auto sx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+      auto sy = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+      out[db][pr] = make_uint4(sx[0], sy[0], sx[1], sy[1]);
     }
+  if (qi < T) {
+    f16* orow = o + ((size_t)b * T + qi) * ldo + h * 64 + 8 * hh;
+#pragma unroll
+    for (int db = 0; db < 2; ++db)
+#pragma unroll
+      for (int pr = 0; pr < 2; ++pr) *reinterpret_cast<uint4*>(orow + db * 32 + 16 * pr) = out[db][pr];
   }
 }
 
-template <int QW, int NW>
+// Merge S split-KV partials: one thread per (sequence*head, query, 8 dims).
+// O = sum_s 2^(m_s - m) O_s / sum_s 2^(m_s - m) l_s, m = max_s m_s.
+__global__ void __launch_bounds__(256) attn_combine_kernel(SplitWs ws, int S, int BH, int H, int T, int ldo,
+                                                           f16* __restrict__ o) {
+  const int id = blockIdx.x * 256 + threadIdx.x;
+  const int d8 = id & 7, rest = id >> 3;
+  const int qi = rest % T, bh = rest / T;
+  if (bh >= BH) return;
+  float m = -INFINITY;
+  for (int s = 0; s < S; ++s) m = fmaxf(m, ws.ml[(((size_t)s * BH + bh) * ws.Tq + qi) * 2]);
+  float lsum = 0.f, acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  for (int s = 0; s < S; ++s) {
+    const size_t row = ((size_t)s * BH + bh) * ws.Tq + qi;
+    const float2 ml = *reinterpret_cast<const float2*>(ws.ml + row * 2);
+    const float w = __builtin_amdgcn_exp2f(ml.x - m);
+    lsum += w * ml.y;
+    const float4 a = *reinterpret_cast<const float4*>(ws.o + row * 64 + 8 * d8);
+    const float4 c = *reinterpret_cast<const float4*>(ws.o + row * 64 + 8 * d8 + 4);
+    acc[0] += w * a.x;
+    acc[1] += w * a.y;
+    acc[2] += w * a.z;
+    acc[3] += w * a.w;
+    acc[4] += w * c.x;
+    acc[5] += w * c.y;
+    acc[6] += w * c.z;
+    acc[7] += w * c.w;
+  }
+  const float inv = 1.f / lsum;
+  f16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) v[j] = (f16)(acc[j] * inv);
+  const int b = bh / H, h = bh - b * H;
+  *reinterpret_cast<f16x8*>(o + ((size_t)b * T + qi) * ldo + h * 64 + 8 * d8) = v;
+}
+
+template <int NW>
 hipError_t run_attn(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T, int Tpad, int ldo,
-                    hipStream_t st) {
+                    float* ws, size_t ws_bytes, int split, hipStream_t st) {
   constexpr int BQ = QW * NW;
-  dim3 grid((T + BQ - 1) / BQ, B * H);
-  hipLaunchKernelGGL((attn_fwd_kernel<QW, NW>), grid, dim3(NW * 64), 0, st, reinterpret_cast<const f16*>(q),
-                     reinterpret_cast<const f16*>(k), reinterpret_cast<const f16*>(vt), reinterpret_cast<f16*>(o), H,
-                     T, Tpad, ldo);
+  const int nqb = (T + BQ - 1) / BQ, nkt = (T + KT - 1) / KT;
+  const auto cq = reinterpret_cast<const f16*>(q);
+  const auto ck = reinterpret_cast<const f16*>(k);
+  const auto cv = reinterpret_cast<const f16*>(vt);
+  const auto co = reinterpret_cast<f16*>(o);
+  if (split > 1 && ws) {
+    SplitWs w;
+    w.Tq = nqb * BQ;
+    w.tiles = (nkt + split - 1) / split;
+    const int S = (nkt + w.tiles - 1) / w.tiles;  // every split non-empty
+    const size_t rows = (size_t)S * B * H * w.Tq;
+    if (S > 1 && rows * 66 * sizeof(float) <= ws_bytes) {
+      w.o = ws;
+      w.ml = ws + rows * 64;
+      hipLaunchKernelGGL((attn_fwd_kernel<NW, true>), dim3(nqb, B * H, S), dim3(NW * 64), 0, st, cq, ck, cv, co, H, T,
+                         Tpad, ldo, w);
+      const hipError_t e = hipGetLastError();
+      if (e != hipSuccess) return e;
+      const long long n = (long long)B * H * T * 8;
+      hipLaunchKernelGGL(attn_combine_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, w, S, B * H, H, T,
+                         ldo, co);
+      return hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL((attn_fwd_kernel<NW, false>), dim3(nqb, B * H), dim3(NW * 64), 0, st, cq, ck, cv, co, H, T, Tpad,
+                     ldo, SplitWs{});
   return hipGetLastError();
 }
 
 }  // namespace
 
+size_t attention_split_ws_bytes(int B, int H, int T) {
+  // the largest split the launcher picks: 8 ways over 128-query workgroups
+  const size_t tq = (size_t)(T + 127) / 128 * 128;
+  return (size_t)8 * B * H * tq * 66 * sizeof(float);
+}
+
 hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T, int Tpad,
-                            int ldo, hipStream_t st) {
+                            int ldo, hipStream_t st, float* ws, size_t ws_bytes) {
   if (B <= 0 || T <= 0) return hipSuccess;
-  if (Tpad % KT || Tpad < ((T + KT - 1) / KT) * KT || (ldo & 3)) return hipErrorInvalidValue;
-  // tuning override: MDE_ATTN_CFG = 32x4 | 16x8 | 16x4 | 16x2 (queries/wave x waves)
-  static const int forced = [] {
-    const char* e = getenv("MDE_ATTN_CFG");
-    if (!e) return 0;
-    if (!strcmp(e, "32x4")) return 1;
-    if (!strcmp(e, "16x8")) return 2;
-    if (!strcmp(e, "16x4")) return 3;
-    if (!strcmp(e, "16x2")) return 4;
-    return 0;
-  }();
-  switch (forced) {
-    case 1: return run_attn<32, 4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
-    case 2: return run_attn<16, 8>(q, k, vt, o, B, H, T, Tpad, ldo, st);
-    case 3: return run_attn<16, 4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
-    case 4: return run_attn<16, 2>(q, k, vt, o, B, H, T, Tpad, ldo, st);
-    default: break;
+  // the 16-B output stores need ldo % 8 == 0 (and a 16-B aligned o)
+  if (Tpad % KT || Tpad < ((T + KT - 1) / KT) * KT || (ldo & 7) || ((uintptr_t)o & 15)) return hipErrorInvalidValue;
+  const int nkt = (T + KT - 1) / KT;
+  // MDE_ATTN_CFG = <waves>[s<split>] ("8", "4", "4s8", ...): tuning override
+  static const char* forced = getenv("MDE_ATTN_CFG");
+  int nw = 0, split = 1;
+  if (forced) {
+    nw = atoi(forced);
+    const char* sp = strchr(forced, 's');
+    split = sp ? atoi(sp + 1) : 1;
   }
-  // measured on MI355X (tools/bench_kernels.py, T 1370, H 6): 128-query
-  // workgroups of 8 waves win once they fill the chip (B 32: 181 us vs 230 us
-  // for 64-query groups); at B 1 the 64-query groups fill more CUs (21 vs 23 us)
-  const long long g128 = (long long)((T + 127) / 128) * B * H;
-  if (g128 >= 256) return run_attn<16, 8>(q, k, vt, o, B, H, T, Tpad, ldo, st);
-  return run_attn<16, 4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
+  if (nw != 4 && nw != 8) {
+    // 256-query workgroups share each K/V^T tile over 8 waves once the grid
+    // fills the chip (2 per CU); smaller grids take 128-query groups and,
+    // below one group per CU, split the keys (>= 3 tiles per split) until
+    // about 512 workgroups run
+    const long long g256 = (long long)((T + 255) / 256) * B * H;
+    const long long g128 = (long long)((T + 127) / 128) * B * H;
+    nw = g256 >= 512 ? 8 : 4;
+    split = 1;
+    if (nw == 4 && g128 < 256)
+      while (split < 8 && g128 * split * 2 <= 640 && nkt >= 3 * split * 2) split *= 2;
+  }
+  if (nw == 8) return run_attn<8>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, split, st);
+  return run_attn<4>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, split, st);
 }
 
 }  // namespace mde

@@ -83,7 +83,16 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3_kernel(const GemmParams p)
   const int Ho = p.oh, Wo = p.ow;
   const int tiles_x = (Wo + TW - 1) / TW, tiles_y = (Ho + TH - 1) / TH;
   const int ntn = (p.N + BN - 1) / BN;
+  // XCD-aware order (as the GEMM): workgroups are dealt round-robin over the
+  // 8 XCDs, so hand each XCD a contiguous run of tiles -- horizontally and
+  // vertically adjacent tiles then share their halo / bilinear source rows in
+  // one L2 instead of each XCD fetching them again (head.output_conv2 at
+  // B=30 fetched ~2x its 168 MB source map without it).  Bijective.
   int bid = blockIdx.x;
+  {
+    const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
+    bid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+  }
   const int tn = bid % ntn;
   bid /= ntn;
   const int tx = bid % tiles_x;
@@ -134,15 +143,16 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3_kernel(const GemmParams p)
           const f16x8 c = *reinterpret_cast<const f16x8*>(base + ((size_t)y1 * p.cw + x0) * p.cc);
           const f16x8 d = *reinterpret_cast<const f16x8*>(base + ((size_t)y1 * p.cw + x1) * p.cc);
 #if MDE_UP_BLEND_F16
-          // packed f16 blend (v_pk_mul_f16 / v_pk_fma_f16, two channels per op)
+          // packed f16 blend in lerp form, a + (b - a) * w (v_pk_add_f16 /
+          // v_pk_fma_f16, two channels per op): the two weights of each axis
+          // sum to exactly 1, so a constant map (or a folded bias) is preserved
           typedef f16 f16x2b __attribute__((ext_vector_type(2)));
-          const f16x2b wx0 = {(f16)lx0, (f16)lx0}, wx1 = {(f16)lx1, (f16)lx1};
-          const f16x2b wy0 = {(f16)ly0, (f16)ly0}, wy1 = {(f16)ly1, (f16)ly1};
+          const f16x2b wx1 = {(f16)lx1, (f16)lx1}, wy1 = {(f16)ly1, (f16)ly1};
 #pragma unroll
           for (int j = 0; j < 8; j += 2) {
             const f16x2b a2 = {a[j], a[j + 1]}, b2 = {bq[j], bq[j + 1]}, c2 = {c[j], c[j + 1]}, d2 = {d[j], d[j + 1]};
-            const f16x2b t0 = a2 * wx0 + b2 * wx1, t1 = c2 * wx0 + d2 * wx1;
-            const f16x2b r = t0 * wy0 + t1 * wy1;
+            const f16x2b t0 = a2 + (b2 - a2) * wx1, t1 = c2 + (d2 - c2) * wx1;
+            const f16x2b r = t0 + (t1 - t0) * wy1;
             v[j] = r[0];
             v[j + 1] = r[1];
           }

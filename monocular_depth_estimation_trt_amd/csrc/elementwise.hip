@@ -212,14 +212,19 @@ __global__ void __launch_bounds__(256) resize_kernel(const f16* __restrict__ in,
   const f16x8 d = *reinterpret_cast<const f16x8*>(base + ((size_t)y1 * iw + x1) * C);
   f16x8 v;
 #if MDE_RESIZE_F16
-  // packed f16 blend, as the up-conv staging (conv.hip) and TensorRT's fp16 Resize
+  // packed f16 blend in lerp form, a + (b - a) * w, as the up-conv staging
+  // (conv.hip): each axis' two weights sum to exactly 1, so the out_conv bias
+  // folded in front of this resize (engine.hip dav2_fusion) passes unchanged
+  // and a constant map stays constant (tests/test_gpu_ops.py::test_resize_constant)
   typedef f16 f16x2r __attribute__((ext_vector_type(2)));
-  const f16x2r wx0 = {(f16)lx0, (f16)lx0}, wx1 = {(f16)lx1, (f16)lx1};
-  const f16x2r wy0 = {(f16)ly0, (f16)ly0}, wy1 = {(f16)ly1, (f16)ly1};
+  (void)lx0;
+  (void)ly0;
+  const f16x2r wx1 = {(f16)lx1, (f16)lx1}, wy1 = {(f16)ly1, (f16)ly1};
 #pragma unroll
   for (int j = 0; j < 8; j += 2) {
     const f16x2r a2 = {a[j], a[j + 1]}, b2 = {bb[j], bb[j + 1]}, c2 = {c[j], c[j + 1]}, d2 = {d[j], d[j + 1]};
-    const f16x2r r = (a2 * wx0 + b2 * wx1) * wy0 + (c2 * wx0 + d2 * wx1) * wy1;
+    const f16x2r t0 = a2 + (b2 - a2) * wx1, t1 = c2 + (d2 - c2) * wx1;
+    const f16x2r r = t0 + (t1 - t0) * wy1;
     v[j] = r[0];
     v[j + 1] = r[1];
   }

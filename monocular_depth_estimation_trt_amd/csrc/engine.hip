@@ -189,6 +189,11 @@ size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
   t.c1 = a.h(bb * s0 * (F / 2));
   t.lncnt = (unsigned*)a.take((bb * e.T / 32 + 1) * 4);  // >= one word per 32-row block
   t.ws = bb * e.T <= 4096 ? a.f(4 * bb * e.T * D) : nullptr;
+  // attention split-KV workspace for the batches whose (head, 128-query)
+  // grid is under one workgroup per CU (launch_attention splits those)
+  const int bsplit = std::min<int>(B, (256 + ((e.T + 127) / 128) * e.H - 1) / (((e.T + 127) / 128) * e.H));
+  t.aws_bytes = bsplit >= 1 ? attention_split_ws_bytes(bsplit, e.H, e.T) : 0;
+  t.aws = t.aws_bytes ? a.f(t.aws_bytes / sizeof(float)) : nullptr;
   if (b) *b = t;
   return a.off;
 }
@@ -270,9 +275,6 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
   int tap = 0;
   char nm[64];
   const bool fuse = fuse_ln_enabled() && (D == 384 || D == 768 || D == 1024);
-  // fc1 + GELU + fc2 + LayerScale residual in one kernel (ViT-S; mlp_fused.hip)
-  const bool fused_mlp = !fuse && mlp_fused_supported(D, cf.mlp_hidden, ldw("b0.fc1.w"), ldw("b0.fc2.w")) &&
-                         mlp_fused_enabled(B * T);
   // fused LayerNorm in a residual GEMM's tail: out1 = LN(g1,b1) (token
   // layout), out2 = final norm into a tap map (cls dropped)
   auto fuse_ln = [&](GemmParams& g, const char* g1, const char* b1, h16* tapdst) {
@@ -328,7 +330,7 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
       gemm(nm, g);
     }
     snprintf(nm, sizeof nm, "block%d.attn", i);
-    step(nm, [&] { return launch_attention(b.Q, b.K, b.Vt, b.O, B, e.H, T, e.Tpad, D, st); });
+    step(nm, [&] { return launch_attention(b.Q, b.K, b.Vt, b.O, B, e.H, T, e.Tpad, D, st, b.aws, b.aws_bytes); });
     {
       GemmParams g = dense(b.O, D, p + "proj.w", B * T, D, D);
       g.emode = E_RESID;
@@ -347,20 +349,7 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
         return launch_layernorm(b.X, b.Hn, w32(p + "ln2.g"), w32(p + "ln2.b"), B * T, D, cf.ln_eps, T, 0, st);
       });
     }
-    if (fused_mlp) {
-      MlpParams mp;
-      mp.A = b.Hn;
-      mp.M = B * T;
-      mp.W1 = w16(p + "fc1.w");
-      mp.b1 = w32(p + "fc1.b");
-      mp.W2 = w16(p + "fc2.w");
-      mp.ldw2 = ldw(p + "fc2.w");
-      mp.b2 = w32(p + "fc2.b");
-      mp.ls2 = w32(p + "ls2");
-      mp.x32 = b.X;
-      snprintf(nm, sizeof nm, "block%d.mlp", i);
-      step(nm, [&] { return launch_mlp_fused(mp, st); });
-    } else {
+    {
       GemmParams g = dense(b.Hn, D, p + "fc1.w", B * T, cf.mlp_hidden, D);
       g.emode = E_STORE;
       g.bias = w32(p + "fc1.b");
@@ -370,7 +359,7 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
       snprintf(nm, sizeof nm, "block%d.fc1", i);
       gemm(nm, g);
     }
-    if (!fused_mlp) {
+    {
       GemmParams g = dense(b.Mh, cf.mlp_hidden, p + "fc2.w", B * T, D, cf.mlp_hidden);
       g.emode = E_RESID;
       g.bias = w32(p + "fc2.b");
@@ -866,6 +855,19 @@ int mde_context_enqueue(mde_context* c, void* stream) {
   }
   GraphKey key{c->batch, c->in, c->out, c->out2};
   auto it = c->graphs.find(key);
+  if (it == c->graphs.end() && (int)c->graphs.size() >= mde_context::kMaxGraphs) {
+    // evict the least recently launched graph; its last replay may still be
+    // running on some caller stream, so drain the device first (rare path)
+    HIP_OR(hipDeviceSynchronize(), "hipDeviceSynchronize (graph eviction)");
+    auto lru = c->graph_used.begin();
+    for (auto u = c->graph_used.begin(); u != c->graph_used.end(); ++u)
+      if (u->second < lru->second) lru = u;
+    auto victim = c->graphs.find(lru->first);
+    hipGraphExecDestroy(victim->second.second);
+    hipGraphDestroy(victim->second.first);
+    c->graphs.erase(victim);
+    c->graph_used.erase(lru);
+  }
   if (it == c->graphs.end()) {
     hipGraph_t g = nullptr;
     hipGraphExec_t ge = nullptr;
@@ -885,6 +887,7 @@ int mde_context_enqueue(mde_context* c, void* stream) {
     }
     it = c->graphs.emplace(key, std::make_pair(g, ge)).first;
   }
+  c->graph_used[key] = ++c->graph_tick;
   HIP_OR(hipGraphLaunch(it->second.second, st), "hipGraphLaunch");
   return MDE_OK;
 }
@@ -1059,24 +1062,6 @@ int mde_op_tap_concat_ln(const float* xa, const float* xb, int nseq, int tokens,
          "tap_concat_ln");
 }
 
-int mde_op_mlp_residual(const void* a, int m, const void* w1, int ldw1, const float* b1, const void* w2, int ldw2,
-                        const float* b2, const float* ls2, float* x32, int dim, int hidden, void* st) {
-  if (!a || !w1 || !b1 || !w2 || !b2 || !ls2 || !x32) return fail(MDE_ERR_ARG, "null argument");
-  if (!mlp_fused_supported(dim, hidden, ldw1, ldw2))
-    return fail(MDE_ERR_ARG, "mde_op_mlp_residual: only dim 384 / hidden 1536 (ViT-S) with dense weights");
-  MlpParams mp;
-  mp.A = (const h16*)a;
-  mp.M = m;
-  mp.W1 = (const h16*)w1;
-  mp.b1 = b1;
-  mp.W2 = (const h16*)w2;
-  mp.ldw2 = ldw2;
-  mp.b2 = b2;
-  mp.ls2 = ls2;
-  mp.x32 = x32;
-  OP_RET(launch_mlp_fused(mp, (hipStream_t)st), "mlp_residual");
-}
-
 int mde_op_layernorm(const float* x, void* y, const float* g, const float* b, int rows, int dim, float eps,
                      int tokens, int skip_cls, void* st) {
   if (!x || !y || !g || !b) return fail(MDE_ERR_ARG, "null argument");
@@ -1153,6 +1138,18 @@ int mde_op_attention(const void* q, const void* k, const void* vt, void* o, int 
   OP_RET(launch_attention((const h16*)q, (const h16*)k, (const h16*)vt, (h16*)o, batch, heads, tokens, tokens_pad,
                           ldo, (hipStream_t)st),
          "attention");
+}
+
+int mde_op_attention_ws(const void* q, const void* k, const void* vt, void* o, int batch, int heads, int tokens,
+                        int tokens_pad, int ldo, void* ws, size_t ws_bytes, void* st) {
+  if (!q || !k || !vt || !o || (!ws && ws_bytes)) return fail(MDE_ERR_ARG, "null argument");
+  OP_RET(launch_attention((const h16*)q, (const h16*)k, (const h16*)vt, (h16*)o, batch, heads, tokens, tokens_pad,
+                          ldo, (hipStream_t)st, (float*)ws, ws_bytes),
+         "attention_ws");
+}
+
+size_t mde_op_attention_ws_bytes(int batch, int heads, int tokens) {
+  return batch > 0 && heads > 0 && tokens > 0 ? attention_split_ws_bytes(batch, heads, tokens) : 0;
 }
 
 int mde_op_patch_embed(const float* img, int batch, int h, int w, const void* wt, int ldw, const float* bias,

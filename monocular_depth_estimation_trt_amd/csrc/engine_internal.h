@@ -35,6 +35,8 @@ struct DAV2Buf {
   h16 *tb, *sb, *ub, *vb, *p4, *p3, *p2, *c1;
   unsigned* lncnt;  // fused-LayerNorm row-block arrival counters (zeroed, self-resetting)
   float* ws;        // fc2 split-K partials [4][B*T][D] (small-batch contexts only, else null)
+  float* aws;       // attention split-KV partials (batches whose grid splits, else null)
+  size_t aws_bytes;
 };
 
 // Depth Pro activations (depth_pro.hip plan_arena_dp).  Token buffers are
@@ -130,7 +132,13 @@ struct mde_context {
   mde::VGBuf v{};
   bool graph_mode = true;
   hipStream_t cap_stream = nullptr;
+  // captured forwards per (batch, io addresses), at most kMaxGraphs of them:
+  // the least recently launched one is destroyed to make room (a caller that
+  // rebinds fresh buffers every call pays a capture, not unbounded growth)
+  static constexpr int kMaxGraphs = 8;
   std::map<mde::GraphKey, std::pair<hipGraph_t, hipGraphExec_t>> graphs;
+  std::map<mde::GraphKey, unsigned long long> graph_used;
+  unsigned long long graph_tick = 0;
   mde_layer_cb prof_cb = nullptr;
   void* prof_user = nullptr;
   std::vector<std::pair<std::string, std::pair<hipEvent_t, hipEvent_t>>> prof_events;

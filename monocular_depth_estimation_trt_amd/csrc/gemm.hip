@@ -551,7 +551,11 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
   if (p.amode == A_DENSE && ((p.lda & 7) || p.lda < p.K)) return hipErrorInvalidValue;
   if (p.amode != A_DENSE && (p.cc & 7)) return hipErrorInvalidValue;
   if ((p.emode == E_STORE || p.emode == E_RESID || p.emode == E_PATCH) && (p.ldo & 7)) return hipErrorInvalidValue;
-  if (p.emode == E_CONVT && (p.cout & 7)) return hipErrorInvalidValue;
+  // E_CONVT stores 16 B per output pixel (f16x8 at pixel*ldo + co): ldo and
+  // the base must keep every such store 16-B aligned (Depth Pro writes into
+  // concat slots, out16 = base + sd0)
+  if (p.emode == E_CONVT && ((p.cout & 7) || (p.ldo & 7) || p.ldo < p.cout || ((uintptr_t)p.out16 & 15)))
+    return hipErrorInvalidValue;
   if (p.emode == E_HEAD && (p.N != 32 || p.amode == A_DENSE)) return hipErrorInvalidValue;
   if (p.amode != A_DENSE && conv_direct_supported(p) && !getenv_im2col() && !prefer_im2col(p))
     return launch_conv3(p, st);
@@ -578,11 +582,6 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
     return launch_splitk_resid(p.partial, S, p.M, p.N, p.bias, p.ls, p.x32, p.ldo, st);
   }
   if (gemm256_eligible(p)) return launch_gemm256(p, st);
-  if (p.amode == A_DENSE && gemm_persistent_enabled() && !p.ln_counter) {
-    // one 256x128 tile per CU per round at least: the persistent pipeline wins
-    const long long tiles = (long long)((p.M + 255) / 256) * ((p.N + 127) / 128);
-    if (tiles >= 256) return launch_gemm_persistent(p, st);
-  }
   switch (p.amode) {
     case A_DENSE:
       switch (p.emode) {

@@ -56,14 +56,11 @@ MDE_DEV void ac_index(float scale, int dst, int in_size, int& i0, int& i1, float
   l0 = 1.f - l1;
 }
 
-// Storage position of key t in a V^T row: inside every 32-key group the keys
-// are ordered [4 keys of sub-tile 0 | 4 keys of sub-tile 1] per 4-key lane
-// slot, so the 8 keys one MFMA lane consumes in P.V ({32g+4h+0..3,
-// 32g+16+4h+0..3}) are one contiguous 16-byte read.
-MDE_DEV int vt_pos(int t) {
-  const int k = t & 31;
-  return (t & ~31) | ((k & 15) >> 2) << 3 | (k >> 4) << 2 | (k & 3);
-}
+// Storage position of key t in a V^T row: bits 2 and 3 of t swapped.  The
+// attention's P.V MFMA (32x32x16, P^T straight from the score accumulator)
+// takes, in lane half h of k-step g, the keys {16g + 4h + 0..3, 16g + 8 + 4h +
+// 0..3}; stored at 16g + 8h + 0..7 they are one contiguous 16-byte read.
+MDE_DEV int vt_pos(int t) { return (t & ~12) | ((t & 4) << 1) | ((t & 8) >> 1); }
 
 // Tile (tm, tn) of the linear workgroup index `bid` (after the XCD remap,
 // which hands each XCD a contiguous run of bids).  gm <= 1: row-major, N

@@ -84,17 +84,16 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st);
 bool conv_direct_supported(const GemmParams& p);
 hipError_t launch_conv3(const GemmParams& p, hipStream_t st);
 
-// Persistent pipelined dense GEMM (gemm_persistent.hip); launch_gemm routes
-// large dense problems here when MDE_GEMM_PERSISTENT=1 (A/B tuning path).
-bool gemm_persistent_enabled();
 // 256x256 phase-pipelined dense GEMM (gemm256.hip) for large token-major
 // problems; launch_gemm routes there when gemm256_eligible() (MDE_GEMM256=0 off).
 bool gemm256_eligible(const GemmParams& p);
 hipError_t launch_gemm256(const GemmParams& p, hipStream_t st);
-hipError_t launch_gemm_persistent(const GemmParams& p, hipStream_t st);
 
+// ws (optional, attention_split_ws_bytes): fp32 workspace for the split-KV
+// path the launcher takes on grids too small to fill the chip (batch 1)
 hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T,
-                            int Tpad, int ldo, hipStream_t st);
+                            int Tpad, int ldo, hipStream_t st, float* ws = nullptr, size_t ws_bytes = 0);
+size_t attention_split_ws_bytes(int B, int H, int T);
 
 hipError_t launch_layernorm(const float* x, h16* y, const float* g, const float* b, int rows, int D,
                             float eps, int T, int skip_cls, hipStream_t st);
@@ -131,17 +130,6 @@ hipError_t launch_cls_rows(float* X, const float* cls, int nseq, int T, int D, h
 hipError_t launch_merge_tokens(const float* x, h16* y, const float* g, const float* b, int D, const DpMerge& m,
                                float eps, hipStream_t st);
 hipError_t launch_fov_final(const h16* in, const float* w, float bias, int K, int B, float* out, hipStream_t st);
-
-// ---- fused ViT-S MLP (mlp_fused.hip) ----
-struct MlpParams {
-  const h16* A = nullptr; int M = 0;                                  // LN output rows [M][384]
-  const h16* W1 = nullptr; const float* b1 = nullptr;                 // fc1 [1536][384]
-  const h16* W2 = nullptr; int ldw2 = 0; const float* b2 = nullptr;   // fc2 [384][ldw2]
-  const float* ls2 = nullptr; float* x32 = nullptr;                   // LayerScale, residual [M][384]
-};
-bool mlp_fused_supported(int dim, int hidden, int ldw1, int ldw2);
-bool mlp_fused_enabled(int M);  // MDE_FUSED_MLP: 0 off, 1 auto (>= 256 row blocks), 2 always
-hipError_t launch_mlp_fused(const MlpParams& p, hipStream_t st);
 
 // ---- VGGT (vggt_ops.hip) ----
 // Token geometry of the q/k rows one qk_norm_rope launch covers: T tokens per

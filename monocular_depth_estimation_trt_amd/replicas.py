@@ -11,8 +11,12 @@ the max-time reduction and the optional result gather -- never RCCL.
 
 from __future__ import annotations
 
+import os
+import socket
+import subprocess
+import sys
 import time
-from typing import Callable, List, Optional, Tuple
+from typing import Callable, List, Optional, Sequence, Tuple
 
 
 def shard(global_batch: int, world: int, rank: int) -> Tuple[int, int]:
@@ -61,3 +65,53 @@ def gather_to_rank0(arr) -> Optional[List]:
     out = [None] * dist.get_world_size() if dist.get_rank() == 0 else None
     dist.gather_object(arr, out, dst=0)
     return out
+
+
+def free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def spawn_local(nprocs: int, script: str, argv: Sequence[str], timeout: Optional[float] = None,
+                env: Optional[dict] = None) -> int:
+    """Run `python script argv...` as nprocs rank processes of one node (the
+    torch.distributed.run environment: RANK, LOCAL_RANK, WORLD_SIZE,
+    LOCAL_WORLD_SIZE, MASTER_ADDR=127.0.0.1, MASTER_PORT) and wait for them.
+    The caller must not have initialised the GPU: the children pick their own
+    device from LOCAL_RANK.  stdout/stderr are inherited (rank 0 prints the
+    result).  If one rank fails the others are terminated; returns the first
+    non-zero exit code, else 0."""
+    if nprocs < 1:
+        raise ValueError("nprocs must be >= 1")
+    port = free_port()
+    base = dict(os.environ if env is None else env)
+    base.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    procs = []
+    for r in range(nprocs):
+        e = dict(base, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(nprocs), LOCAL_WORLD_SIZE=str(nprocs),
+                 MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, script, *argv], env=e))
+    deadline = None if timeout is None else time.monotonic() + timeout
+    rc = 0
+    live = list(procs)
+    while live:
+        for p in list(live):
+            code = p.poll()
+            if code is None:
+                continue
+            live.remove(p)
+            if code != 0 and rc == 0:
+                rc = code
+                for q in live:
+                    q.terminate()
+        if deadline is not None and time.monotonic() > deadline and live:
+            for q in live:
+                q.kill()
+            rc = rc or 124
+        time.sleep(0.05)
+    for p in procs:
+        p.wait()
+    return rc

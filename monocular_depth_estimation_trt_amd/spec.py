@@ -1,7 +1,17 @@
-"""Read and validate models/<name>/spec.json -- the drop-in for the
-reference's `core/spec.py` (:39-111): same schema, same REQUIRED keys, same
-SpecError on a malformed spec, stdlib-only.  The reference's own spec files
-load with it unchanged (tests/test_spec_loader.py)."""
+"""models/<name>/spec.json reader for the HIP engine's drivers.
+
+Contract (what the reference's `core/spec.py` promises its callers, :39-111):
+the same schema number and required keys, `SpecError` (a ValueError) naming
+the file and the first rule a spec breaks, `load` by model name or by path,
+`load_all` keyed by folder name, `size_of` defaulting to the first build
+target, `caveats`.  The reference's own spec files load here unchanged
+(tests/test_spec_loader.py).  Standard library only, so a driver can read a
+spec without importing torch or the engine.
+
+The checks are a table of (rule, predicate) pairs run in order; the first
+failing predicate raises.  On top of the reference contract this module maps
+a DA-V2-family spec to the engine build config (`model_config_of`).
+"""
 
 import json
 import os
@@ -11,10 +21,45 @@ MODELS = os.path.join(HERE, "models")
 
 SCHEMA = 1
 REQUIRED = ("schema", "name", "env", "input", "outputs", "profiles", "build_targets")
+INPUT_KEYS = ("name", "rank", "dtype", "layout")
+OUTPUT_KEYS = ("name", "meaning")
 
 
 class SpecError(ValueError):
-    pass
+    """A spec.json that breaks the schema."""
+
+
+def _is_hw(v):
+    return isinstance(v, list) and len(v) == 2 and all(isinstance(x, int) and x > 0 for x in v)
+
+
+def _rules(spec):
+    """Yield (message, ok) in check order; messages keep the reference's
+    wording for the conditions its tests match on."""
+    absent = [k for k in REQUIRED if k not in spec]
+    yield f"missing {absent}", not absent
+    yield f"schema {spec['schema']}, expected {SCHEMA}", spec["schema"] == SCHEMA
+    inp = spec["input"]
+    for k in INPUT_KEYS:
+        yield f"input.{k} missing", k in inp
+    yield f"input.rank {inp['rank']} is not 4 or 5", inp["rank"] in (4, 5)
+    yield "outputs is empty", bool(spec["outputs"])
+    for out in spec["outputs"]:
+        for k in OUTPUT_KEYS:
+            yield f"output.{k} missing in {out}", k in out
+    yield "profiles is empty", bool(spec["profiles"])
+    for name, prof in spec["profiles"].items():
+        yield f"profile {name} size must be [h, w], got {prof.get('size')}", _is_hw(prof.get("size"))
+    yield "build_targets is empty -- nothing would be built", bool(spec["build_targets"])
+    for tgt in spec["build_targets"]:
+        yield f"build target {tgt} names an unknown profile", tgt.get("profile") in spec["profiles"]
+
+
+def validate(spec, where="<spec>"):
+    for msg, ok in _rules(spec):
+        if not ok:
+            raise SpecError(f"{where}: {msg}")
+    return spec
 
 
 def path_for(name, models_dir=None):
@@ -22,64 +67,28 @@ def path_for(name, models_dir=None):
 
 
 def load(name_or_path, models_dir=None):
-    """One spec by model name (under models_dir) or by path to a .json."""
-    p = name_or_path if name_or_path.endswith(".json") else path_for(name_or_path, models_dir)
-    if not os.path.isfile(p):
-        raise SpecError(f"no spec at {p}")
-    with open(p, encoding="utf-8") as f:
-        spec = json.load(f)
-    validate(spec, p)
-    return spec
+    """One spec, by model folder name (under models_dir) or by a .json path."""
+    path = name_or_path if name_or_path.endswith(".json") else path_for(name_or_path, models_dir)
+    if not os.path.isfile(path):
+        raise SpecError(f"no spec at {path}")
+    with open(path, encoding="utf-8") as f:
+        return validate(json.load(f), path)
 
 
 def load_all(models_dir=None):
+    """{folder name: spec} for every folder of models_dir holding a spec.json."""
     root = models_dir or MODELS
-    out = {}
     if not os.path.isdir(root):
-        return out
-    for d in sorted(os.listdir(root)):
-        p = path_for(d, root)
-        if os.path.isfile(p):
-            out[d] = load(p)
-    return out
-
-
-def validate(spec, where="<spec>"):
-    missing = [k for k in REQUIRED if k not in spec]
-    if missing:
-        raise SpecError(f"{where}: missing {missing}")
-    if spec["schema"] != SCHEMA:
-        raise SpecError(f"{where}: schema {spec['schema']}, expected {SCHEMA}")
-    inp = spec["input"]
-    for k in ("name", "rank", "dtype", "layout"):
-        if k not in inp:
-            raise SpecError(f"{where}: input.{k} missing")
-    if inp["rank"] not in (4, 5):
-        raise SpecError(f"{where}: input.rank {inp['rank']} is not 4 or 5")
-    if not spec["outputs"]:
-        raise SpecError(f"{where}: outputs is empty")
-    for o in spec["outputs"]:
-        for k in ("name", "meaning"):
-            if k not in o:
-                raise SpecError(f"{where}: output.{k} missing in {o}")
-    if not spec["profiles"]:
-        raise SpecError(f"{where}: profiles is empty")
-    for pname, prof in spec["profiles"].items():
-        size = prof.get("size")
-        if not (isinstance(size, list) and len(size) == 2 and all(isinstance(v, int) and v > 0 for v in size)):
-            raise SpecError(f"{where}: profile {pname} size must be [h, w], got {size}")
-    if not spec["build_targets"]:
-        raise SpecError(f"{where}: build_targets is empty")
-    for t in spec["build_targets"]:
-        if t.get("profile") not in spec["profiles"]:
-            raise SpecError(f"{where}: build target {t} names an unknown profile")
-    return spec
+        return {}
+    names = sorted(d for d in os.listdir(root) if os.path.isfile(path_for(d, root)))
+    return {d: load(path_for(d, root)) for d in names}
 
 
 def size_of(spec, profile=None):
-    if profile is None:
-        profile = spec["build_targets"][0]["profile"]
-    return tuple(spec["profiles"][profile]["size"])
+    """(h, w) of a profile; the first build target's profile by default."""
+    prof = profile if profile is not None else spec["build_targets"][0]["profile"]
+    h, w = spec["profiles"][prof]["size"]
+    return (h, w)
 
 
 def caveats(spec):

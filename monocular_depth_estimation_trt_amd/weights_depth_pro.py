@@ -40,6 +40,9 @@ VIT = {
     "dinov2l16_384": dict(embed_dim=1024, depth=24, num_heads=16),
     # reduced widths with the same 384/16 token geometry: parity fixtures
     "tiny": dict(embed_dim=128, depth=4, num_heads=2),
+    # the real widths (D 1024, 16 heads, decoder 256, scaled dims 1024/1024/512)
+    # with 4 instead of 24 blocks per encoder: the full-width parity fixture
+    "dinov2l16_384_shallow": dict(embed_dim=1024, depth=4, num_heads=16),
 }
 
 
@@ -52,6 +55,8 @@ def depth_pro_config(preset: str = "dinov2l16_384", use_fov: bool = True, **over
     cfg = dict(VIT[preset])
     if preset == "tiny":
         cfg.update(hooks=[3, 1], inter_dims=[128, 128], scaled_dims=[256, 256, 128], fusion=128)
+    elif preset == "dinov2l16_384_shallow":
+        cfg.update(hooks=[3, 1], inter_dims=[256, 256], scaled_dims=[1024, 1024, 512], fusion=256)
     else:
         cfg.update(hooks=[11, 5], inter_dims=[256, 256], scaled_dims=[1024, 1024, 512], fusion=256)
     cfg.update(family="depth_pro", encoder=preset, patch=16, vit_size=384, img=1536,

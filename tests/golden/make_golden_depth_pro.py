@@ -15,7 +15,12 @@ with narrow layers.  The input (synthetic_images, seeds 200..) is regenerated
 by the tests, not stored; outputs are stored subsampled every 8th pixel with
 full-map statistics, plus the FOV scalars.
 
-  depth_pro_tiny_b2.npz   B=2, use_fov=True
+  depth_pro_tiny_b2.npz          B=2, use_fov=True
+  depth_pro_shallow_b1.npz       B=1, use_fov=True, the "dinov2l16_384_shallow"
+                                 preset: the real widths (D 1024, 16 heads,
+                                 decoder 256, scaled dims 1024/1024/512) with 4
+                                 blocks per encoder; output every 2nd pixel in
+                                 f16 (768x768) + full-map statistics
 """
 
 from __future__ import annotations
@@ -49,7 +54,7 @@ def hf_config(cfg: dict):
         image_model_config=dict(sub), patch_model_config=dict(sub), fov_model_config=dict(sub))
 
 
-def run_case(name, preset, batch, use_fov=True, seed=4321, first_seed=200):
+def run_case(name, preset, batch, use_fov=True, seed=4321, first_seed=200, sub=8, f16=False):
     from transformers import DepthProForDepthEstimation
     cfg = WD.depth_pro_config(preset, use_fov=use_fov)
     sd = WD.synthetic_state_dict(cfg, seed)
@@ -72,7 +77,11 @@ def run_case(name, preset, batch, use_fov=True, seed=4321, first_seed=200):
                batch=np.array(batch), use_fov=np.array(int(use_fov)),
                weights_sha256=np.array(WD.state_dict_digest(sd)),
                out_min=np.float64(y_hf.min()), out_max=np.float64(y_hf.max()), out_mean=np.float64(y_hf.mean()),
-               out_std=np.float64(y_hf.std()), output_hf_sub8=y_hf[:, ::8, ::8].astype(np.float32))
+               out_std=np.float64(y_hf.std()))
+    if f16:
+        rec[f"output_hf_sub{sub}_f16"] = y_hf[:, ::sub, ::sub].astype(np.float16)
+    else:
+        rec[f"output_hf_sub{sub}"] = y_hf[:, ::sub, ::sub].astype(np.float32)
     if use_fov:
         e = np.abs(fov_hf - fov_or.numpy()).max()
         print(f"  fov HF {fov_hf}  oracle {fov_or.numpy()}  max_abs {e:.3e}")
@@ -81,6 +90,13 @@ def run_case(name, preset, batch, use_fov=True, seed=4321, first_seed=200):
     np.savez_compressed(os.path.join(HERE, f"{name}.npz"), **rec)
 
 
+CASES = {
+    "depth_pro_tiny_b2": dict(preset="tiny", batch=2),
+    "depth_pro_shallow_b1": dict(preset="dinov2l16_384_shallow", batch=1, first_seed=300, sub=2, f16=True),
+}
+
 if __name__ == "__main__":
     torch.set_num_threads(min(8, os.cpu_count() or 1))
-    run_case("depth_pro_tiny_b2", "tiny", 2)
+    for name, kw in CASES.items():
+        if len(sys.argv) == 1 or name in sys.argv[1:]:
+            run_case(name, **kw)

@@ -36,9 +36,9 @@ def op(name: str, *args) -> None:
 
 
 def vt_pos(t):
-    """Key permutation of the V^T layout (csrc/mde_device.h vt_pos)."""
-    k = t & 31
-    return (t & ~31) | (((k & 15) >> 2) << 3) | ((k >> 4) << 2) | (k & 3)
+    """Key permutation of the V^T layout (csrc/mde_device.h vt_pos): bits 2
+    and 3 of t swapped."""
+    return (t & ~12) | ((t & 4) << 1) | ((t & 8) >> 1)
 
 
 def vt_perm(T: int) -> torch.Tensor:

@@ -47,6 +47,24 @@ def test_oracle_matches_hf_golden():
     np.testing.assert_allclose(fov.numpy(), z["fov_hf"], atol=1e-5, rtol=1e-5)
 
 
+def test_oracle_matches_hf_golden_real_widths():
+    """The "dinov2l16_384_shallow" preset: the real Depth Pro widths (D 1024,
+    16 heads, decoder 256, scaled dims 1024/1024/512), 4 blocks per encoder,
+    B=1 at 1536^2 -- the full-width fixture the GPU test checks the engine on."""
+    z = np.load(os.path.join(GOLDEN, "depth_pro_shallow_b1.npz"), allow_pickle=False)
+    cfg = WD.depth_pro_config(str(z["preset"]), use_fov=bool(int(z["use_fov"])))
+    assert (cfg["embed_dim"], cfg["num_heads"], cfg["fusion"], cfg["scaled_dims"]) == (1024, 16, 256, [1024, 1024, 512])
+    sd = WD.synthetic_state_dict(cfg, int(z["seed"]))
+    assert WD.state_dict_digest(sd) == str(z["weights_sha256"]), "weight generator drifted"
+    x = WD.synthetic_images(1, cfg["img"], first_seed=int(z["input_first_seed"]))
+    torch.set_num_threads(min(8, os.cpu_count() or 1))
+    y, fov = depth_pro_ref.forward(depth_pro_ref.to_torch(sd), cfg, x)
+    ref = z["output_hf_sub2_f16"].astype(np.float32)
+    np.testing.assert_allclose(y.numpy()[:, ::2, ::2], ref, atol=1e-2, rtol=1e-3)   # f16 storage
+    assert abs(float(y.mean()) - float(z["out_mean"])) < 1e-4
+    np.testing.assert_allclose(fov.numpy(), z["fov_hf"], atol=1e-5, rtol=1e-5)
+
+
 def test_merge_geometry():
     """The 1536 geometry: every merged level comes out at its target size, so
     HF's bilinear resize after the merge is the identity."""

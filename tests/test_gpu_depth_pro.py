@@ -131,6 +131,28 @@ def test_graph_equals_eager_and_batch_consistency(tiny_case):
     assert np.array_equal(y1[0], yg[1]) and np.array_equal(f1[0], fg[1])
 
 
+def test_engine_real_widths_vs_hf_golden(gpu):
+    """Depth Pro at its real widths (D 1024 / 16 heads / decoder 256 / scaled
+    dims 1024-1024-512, the "dinov2l16_384_shallow" preset: 4 blocks per
+    encoder), B=1 at 1536^2, canonical inverse depth + fov_deg, against the
+    HF golden (every 2nd pixel, f16).  Same bars as the tiny preset."""
+    z = np.load(os.path.join(GOLDEN, "depth_pro_shallow_b1.npz"), allow_pickle=False)
+    cfg = WD.depth_pro_config(str(z["preset"]))
+    sd = WD.synthetic_state_dict(cfg, int(z["seed"]))
+    assert WD.state_dict_digest(sd) == str(z["weights_sha256"])
+    x = WD.synthetic_images(1, cfg["img"], first_seed=int(z["input_first_seed"]))
+    y, fov = run_engine(pack_depth_pro.pack_bytes(sd, cfg), x)
+    ref = z["output_hf_sub2_f16"].astype(np.float32)
+    m = depth_metrics(y[:, ::2, ::2], ref)
+    print("depth_pro real widths B=1", m, "fov", fov, z["fov_hf"], "full mean", float(y.mean()), float(z["out_mean"]))
+    assert np.isfinite(y).all() and np.isfinite(fov).all()
+    assert m["rel_mean"] <= 1e-2, m
+    assert m["corr"] >= 0.999, m
+    assert m["max_abs"] <= 0.03 * float(np.abs(ref).max()), m
+    assert abs(float(y.mean()) - float(z["out_mean"])) <= 1e-2 * abs(float(z["out_mean"]))
+    assert np.all(np.abs(fov - z["fov_hf"]) <= 2e-2 + 1e-2 * np.abs(z["fov_hf"])), (fov, z["fov_hf"])
+
+
 def test_engine_rejects_bad_shapes(tiny_case):
     cfg, sd, x, ref, fov_ref, blob = tiny_case
     eng = Engine.from_bytes(blob, 0, profile=((1, 3, 1536, 1536),) * 3)

@@ -2,10 +2,15 @@
 and the committed golden fixtures (HF-pinned, tests/golden/make_golden.py).
 
 Tolerance (north_star: "fp16 depth maps ... within a stated per-pixel
-tolerance"): the engine computes with fp16 operands and fp32 accumulation, so
-against the fp32 reference we require
-    rel_mean <= 0.5 %,  Pearson corr >= 0.9995,
-    per pixel |d - d_ref| <= 0.02 * max_depth (0.4 m for the metric head)
+tolerance"): the engine computes with fp16 operands and fp32 accumulation.
+Against the fp32 reference (2-3x the error measured on MI355X,
+profiles/r02_gpu_tests.log: ViT-S 518 rel 6.1e-4 / 0.028 m, ViT-L 518 rel
+3.1e-4 / 0.029 m):
+    ViT-S/B/L:      rel_mean <= 0.15 %,  max |d - d_ref| <= 0.003 * max_depth
+    relative heads: rel_mean <= 0.5 % (ReLU output: mean |ref| is small)
+    all:            Pearson corr >= 0.9999
+(0.06 m for the metric head's 20 m).  The 518x518 HF goldens are
+stored in f16 (<= 7.9e-3 quantisation), added to the max_abs bound there.
 The reference's own TensorRT fp16 engine measured rel_mean 0.170 %, max_abs
 0.0239 m, corr 0.99998 against its fp32 ONNX (reports/accuracy.json:32-35).
 Shape and index handling must be exact (output [B,H,W], tap indices, NHWC
@@ -26,9 +31,12 @@ from monocular_depth_estimation_trt_amd.engine import Engine
 
 pytestmark = pytest.mark.gpu
 
-REL_MEAN = 5e-3
-CORR = 0.9995
-PIX_FRAC = 0.02
+CORR = 0.9999
+TOL = {"vits": (1.5e-3, 0.003), "vitb": (1.5e-3, 0.003), "vitl": (1.5e-3, 0.003),  # (rel_mean, max_abs / max_depth)
+       # relative heads end in a ReLU: most of the map sits near 0, so the same
+       # absolute error is a larger fraction of mean |ref| (measured 1.9e-3)
+       "relative": (5e-3, 0.003)}
+F16_Q = 7.9e-3   # f16 storage quantisation of the 518^2 goldens
 
 
 def run_engine(blob, x: np.ndarray, graph=True, max_batch=None):
@@ -50,13 +58,14 @@ def run_engine(blob, x: np.ndarray, graph=True, max_batch=None):
     return y
 
 
-def check(y, ref, max_depth, what):
+def check(y, ref, max_depth, what, encoder="vits", extra_abs=0.0):
+    rel_bar, abs_frac = TOL[encoder]
     m = depth_metrics(y, ref)
-    print(what, m)
+    print(what, m, flush=True)
     assert np.isfinite(y).all(), what
-    assert m["rel_mean"] <= REL_MEAN, (what, m)
+    assert m["rel_mean"] <= rel_bar, (what, m)
     assert m["corr"] >= CORR, (what, m)
-    assert m["max_abs"] <= PIX_FRAC * max_depth, (what, m)
+    assert m["max_abs"] <= abs_frac * max_depth + extra_abs, (what, m)
     return m
 
 
@@ -73,21 +82,25 @@ def test_engine_vs_golden_98(gpu, name):
     ref = z["output_hf"]
     assert y.shape == ref.shape
     md = cfg["max_depth"] if dt == "metric" else max(float(np.abs(ref).max()), 1e-3)
-    check(y, ref, md, name)
+    check(y, ref, md, name, enc if dt == "metric" else "relative")
 
 
-def test_engine_vs_golden_518(gpu):
-    z = np.load(os.path.join(GOLDEN, "dav2_vits_metric_518.npz"), allow_pickle=False)
-    cfg = weights.model_config("vits", "metric")
-    sd = weights.synthetic_state_dict(cfg, 1234)
+@pytest.mark.parametrize("name,encoder", [("dav2_vits_metric_518", "vits"), ("dav2_vitl_metric_518", "vitl")])
+def test_engine_vs_golden_518(gpu, name, encoder):
+    """Full 518x518 map at B=1 against HF.  ViT-L at B=1 is BASELINE config
+    3's per-GPU unit: its fc2 runs as 2 split-K slices (engine.hip split_k)."""
+    z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    cfg = weights.model_config(encoder, "metric")
+    sd = weights.synthetic_state_dict(cfg, int(z["seed"]))
+    assert weights.state_dict_digest(sd) == str(z["weights_sha256"]), "synthetic weight generator drifted"
     blob = pack.pack_bytes(sd, cfg, 518, 518)
     x = weights.synthetic_images(1, 518, 518, first_seed=int(z["input_first_seed"]))
     y = run_engine(blob, x)
     assert y.shape == (1, 518, 518)
-    check(y[:, ::7, ::7], z["output_hf_sub7"], 20.0, "518 subsampled vs HF golden")
-    # full-map statistics recorded from HF
-    assert abs(float(y.mean()) - float(z["out_mean"])) < 0.01 * abs(float(z["out_mean"]))
-    assert abs(float(y.std()) - float(z["out_std"])) < 0.02 * float(z["out_std"])
+    check(y, z["output_hf_f16"].astype(np.float32), 20.0, f"{name} B=1 vs HF golden (full map)", encoder,
+          extra_abs=F16_Q)
+    assert abs(float(y.mean()) - float(z["out_mean"])) < 2e-3 * abs(float(z["out_mean"]))
+    assert abs(float(y.std()) - float(z["out_std"])) < 5e-3 * float(z["out_std"])
 
 
 def test_engine_vs_oracle_518_full(gpu):
@@ -98,6 +111,18 @@ def test_engine_vs_oracle_518_full(gpu):
     ref = dav2_ref.forward(dav2_ref.to_torch(sd), cfg, x).numpy()
     y = run_engine(pack.pack_bytes(sd, cfg, 518, 518), x)
     check(y, ref, 20.0, "518 B=2 vs oracle")
+
+
+def test_engine_vitl_518_b2_vs_oracle(gpu):
+    """ViT-L 518x518, B=2 (unsplit fc2: 688 64^2 tiles) against the oracle."""
+    from oracle import dav2_ref
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    cfg = weights.model_config("vitl", "metric")
+    sd = weights.synthetic_state_dict(cfg, 77)
+    x = weights.synthetic_images(2, 518, 518, first_seed=40)
+    ref = dav2_ref.forward(dav2_ref.to_torch(sd), cfg, x).numpy()
+    y = run_engine(pack.pack_bytes(sd, cfg, 518, 518), x)
+    check(y, ref, 20.0, "vitl 518 B=2 vs oracle", "vitl")
 
 
 def test_engine_nonsquare_vs_oracle(gpu):
@@ -128,15 +153,16 @@ def test_batch_and_graph_consistency(gpu):
         assert m["max_abs"] < 0.05 and m["rel_mean"] < 1e-3, (i, m)
 
 
-def test_fc2_splitk_matches_unsplit(gpu):
-    """Small-batch contexts split fc2's K loop four ways (engine.hip, fc2);
-    the slices are summed in order, so the result is deterministic and equal
-    to the unsplit GEMM up to fp32 reassociation."""
-    import os
-    cfg = weights.model_config("vits", "metric")
+@pytest.mark.parametrize("encoder,size", [("vits", 98), ("vitl", 518)])
+def test_fc2_splitk_matches_unsplit(gpu, encoder, size):
+    """Small-batch contexts split fc2's K loop (engine.hip split_k: ViT-S at
+    98^2 4 slices, ViT-L at 518^2 2 slices -- config 3's B=1); the slices are
+    summed in order, so the result is deterministic and equal to the unsplit
+    GEMM up to fp32 reassociation."""
+    cfg = weights.model_config(encoder, "metric")
     sd = weights.synthetic_state_dict(cfg, 5)
-    blob = pack.pack_bytes(sd, cfg, 98, 98)
-    x = weights.synthetic_images(1, 98, 98, first_seed=21)
+    blob = pack.pack_bytes(sd, cfg, size, size)
+    x = weights.synthetic_images(1, size, size, first_seed=21)
     y_split = run_engine(blob, x, graph=True)
     assert np.array_equal(y_split, run_engine(blob, x, graph=False)), "split-K must be deterministic"
     os.environ["MDE_SPLITK"] = "0"
@@ -145,5 +171,7 @@ def test_fc2_splitk_matches_unsplit(gpu):
     finally:
         os.environ.pop("MDE_SPLITK", None)
     m = depth_metrics(y_split, y_plain)
-    print("split-K vs unsplit", m)
-    assert m["max_abs"] < 0.05 and m["rel_mean"] < 1e-3, m
+    print(f"split-K vs unsplit {encoder} {size}", m)
+    # the fp32 reassociation is amplified by the downstream f16 roundings
+    # (measured ViT-S 0.026 m / 6.6e-4, ViT-L 0.036 m / 6.2e-4)
+    assert m["max_abs"] < 0.08 and m["rel_mean"] < 1.5e-3, m

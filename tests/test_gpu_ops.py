@@ -31,8 +31,9 @@ def f16(t, dev):
 
 @pytest.mark.parametrize("m,n,k,act", [(300, 200, 96, 0), (1370, 1152, 384, 0), (777, 1536, 384, 2),
                                        (64, 48, 48, 1), (5, 32, 64, 1), (2048, 384, 1536, 0),
-                                       # >= 256 tiles of 256x128: the persistent pipelined kernel
-                                       (16384, 1536, 384, 2), (33000, 1024, 200, 1), (65537, 512, 64, 0)])
+                                       (16384, 1536, 384, 2), (33000, 1024, 200, 1), (65537, 512, 64, 0),
+                                       # K >= 768 in whole rounds of 256 256^2 tiles: gemm256 (gemm256_eligible)
+                                       (20480, 4096, 1024, 2), (16384, 1024, 4096, 0)])
 def test_linear(gpu, m, n, k, act):
     a, w, b = rn(m, k), rn(n, k, scale=k ** -0.5), rn(n, scale=0.1)
     a16, w16 = a.half().float(), w.half().float()
@@ -61,7 +62,9 @@ def test_linear_residual(gpu, m, n, k):
     close(xg, ref, 2e-3, 2e-3, "linear_residual")
 
 
-@pytest.mark.parametrize("B,T,H", [(2, 50, 6), (16, 1370, 6)])
+@pytest.mark.parametrize("B,T,H", [(2, 50, 6), (16, 1370, 6),
+                                   # D 1024, 75 x 12 tiles of 256^2 (>= 80 % of 4 rounds): gemm256 E_QKV
+                                   (14, 1370, 16)])
 def test_qkv_layout(gpu, B, T, H):
     D = 64 * H
     Tp = -(-T // 64) * 64
@@ -113,6 +116,34 @@ def test_attention(gpu, B, H, T):
     o = torch.empty(B * T, H * 64, dtype=torch.float16, device=gpu)
     op("mde_op_attention", ptr(qg), ptr(kg), ptr(vtg), ptr(o), B, H, T, Tp, H * 64, stream())
     close(o, ref, 2e-2, 5e-3, f"attention B{B} H{H} T{T}")
+
+
+@pytest.mark.parametrize("B,H,T,spiky", [(1, 6, 1370, False), (1, 16, 1370, False), (1, 2, 700, True),
+                                         (2, 6, 1370, False)])
+def test_attention_split_kv(gpu, B, H, T, spiky):
+    """Batch-1 grids split the key range (launch_attention; 4 ways at 6 x
+    1370, 2 at 16 x 1370) and merge the fp32 partials (attn_combine_kernel);
+    B=2 at 6 heads stays unsplit through the same entry point."""
+    Tp = -(-T // 64) * 64
+    q = rn(B * H, T, 64) * 0.125 * 2.0 * LOG2E
+    k = rn(B * H, T, 64) * 2.0
+    if spiky:  # a dominant key late in the row, and one in another split
+        k[:, T - 10] = q.mean(1) * 60.0
+        k[:, 3] = q.mean(1) * 30.0
+    v = rn(B * H, T, 64)
+    ref = attn_ref(q, k, v).reshape(B, H, T, 64).permute(0, 2, 1, 3).reshape(B * T, H * 64)
+    qg = torch.zeros(B * H, Tp, 64, dtype=torch.float16, device=gpu)
+    kg = torch.zeros_like(qg)
+    vtg = torch.zeros(B * H, 64, Tp, dtype=torch.float16, device=gpu)
+    qg[:, :T], kg[:, :T] = q.half().to(gpu), k.half().to(gpu)
+    vtg[:, :, vt_perm(T).to(gpu)] = v.transpose(1, 2).half().to(gpu)
+    from monocular_depth_estimation_trt_amd import _lib
+    nbytes = _lib.lib().mde_op_attention_ws_bytes(B, H, T)
+    assert nbytes > 0
+    ws = torch.empty(nbytes // 4, dtype=torch.float32, device=gpu)
+    o = torch.empty(B * T, H * 64, dtype=torch.float16, device=gpu)
+    op("mde_op_attention_ws", ptr(qg), ptr(kg), ptr(vtg), ptr(o), B, H, T, Tp, H * 64, ptr(ws), nbytes, stream())
+    close(o, ref, 2e-2, 5e-3, f"attention split-KV B{B} H{H} T{T}")
 
 
 def test_attention_spiky_rows(gpu):
@@ -208,7 +239,9 @@ def test_conv3x3_up(gpu, B, sh, sw, uh, uw, cin, cout):
 
 
 @pytest.mark.parametrize("s,cin,B,h,w", [(4, 48, 2, 7, 9), (2, 96, 2, 7, 9), (4, 256, 2, 7, 9),
-                                        (4, 48, 32, 37, 37), (2, 512, 8, 37, 37)])
+                                        (4, 48, 32, 37, 37), (2, 512, 8, 37, 37),
+                                        # M 16384, N 4096, K 1024: gemm256's LDS-staged E_CONVT epilogue
+                                        (2, 1024, 4, 64, 64)])
 def test_conv_transpose(gpu, s, cin, B, h, w):
     cout = cin
     x = rn(B, cin, h, w)
@@ -230,6 +263,18 @@ def test_resize(gpu, ih, iw, oh, ow, c):
     out = torch.empty(B, oh, ow, c, dtype=torch.float16, device=gpu)
     op("mde_op_resize_bilinear", ptr(nhwc(x).half().to(gpu)), B, ih, iw, c, oh, ow, ptr(out), stream())
     close(nchw(out), ref, 1e-2, 1e-2, "resize")
+
+
+def test_resize_constant_map(gpu):
+    """The blend's weights sum to exactly 1 on each axis (lerp form), so a
+    constant map -- e.g. the out_conv bias folded before the fusion resize --
+    comes out bit-exact."""
+    B, c, ih, iw, oh, ow = 2, 64, 19, 23, 37, 45
+    vals = torch.tensor([0.1, -3.7, 1234.0, 6.1e-5])
+    x = vals.repeat(c // 4).view(1, c, 1, 1).expand(B, c, ih, iw).contiguous()
+    out = torch.empty(B, oh, ow, c, dtype=torch.float16, device=gpu)
+    op("mde_op_resize_bilinear", ptr(nhwc(x).half().to(gpu)), B, ih, iw, c, oh, ow, ptr(out), stream())
+    assert torch.equal(nchw(out).cpu(), x.half()[:, :, :1, :1].expand(B, c, oh, ow))
 
 
 @pytest.mark.parametrize("metric", [1, 0])
