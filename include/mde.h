@@ -144,6 +144,9 @@ int mde_rt_event_elapsed_ms(float* ms, void* start, void* end);
  * [Npad][ldw] f16 row-major (K contiguous), rows >= N zero, ldw % 64 == 0,
  * ldw >= K rounded up to 64, Npad a multiple of 128; N % 8 == 0.  Activation maps are
  * NHWC f16.  act: 0 none, 1 ReLU, 2 GELU(erf). */
+/* The same over an f16 residual stream (precision "fp16" engines): x_f16 [rows][dim]. */
+int mde_op_layernorm_f16(const void* x_f16, void* y_f16, const float* gamma, const float* beta, int rows, int dim,
+                         float eps, int tokens, int skip_cls, void* stream);
 int mde_op_layernorm(const float* x, void* y_f16, const float* gamma, const float* beta, int rows, int dim,
                      float eps, int tokens, int skip_cls, void* stream);
 int mde_op_linear(const void* a_f16, int lda, const void* w_f16, int ldw, int m, int n, int k,

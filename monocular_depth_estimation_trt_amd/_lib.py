@@ -83,6 +83,7 @@ PROTOTYPES = {
     "mde_rt_event_record": [c_void_p, c_void_p],
     "mde_rt_event_elapsed_ms": [P(c_float), c_void_p, c_void_p],
     "mde_op_layernorm": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_int, c_int, c_void_p],
+    "mde_op_layernorm_f16": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_int, c_int, c_void_p],
     "mde_op_linear": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int,
                       c_void_p],
     "mde_op_linear_residual": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,

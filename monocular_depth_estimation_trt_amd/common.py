@@ -165,8 +165,14 @@ def get_engine(onnx_file_path, engine_file_path="", precision="fp32", dynamic_in
     [B, S, 3, H, W] shapes, S fixed).
     `frames` (VGGT): the frame count S the engine is packed for (default 1,
     or the S of the dynamic shapes).
-    `precision`: "fp16" (the engine's arithmetic: f16 operands, fp32
-    accumulation/statistics).  "fp32" raises -- there is no fp32 engine.
+    `precision` (DA-V2): "fp16" -- f16 MFMA operands and activations, the
+    residual stream kept in f16 (the reference's fp16 TensorRT engine); "fp32"
+    (the reference's default) -- the residual stream, LayerNorm / softmax
+    statistics and every accumulation in fp32 with f16 MFMA operands: a
+    10-bit mantissa, the precision of the TF32 tensor-core path the
+    reference's TensorRT fp32 build takes by default (core/common.py:207-218
+    sets no flag that would disable it).  There is no fp32-operand engine.
+    Depth Pro / VGGT engines always keep an fp32 residual stream.
     `input_format` "uint8_nhwc" packs the reference's uint8 preamble
     (core/onnx_tools.py:87-219): the input binding becomes "image_u8",
     uint8 [B,H,W,3], normalised on the device.
@@ -175,11 +181,8 @@ def get_engine(onnx_file_path, engine_file_path="", precision="fp32", dynamic_in
         raise ValueError(f"[MDET] input_format must be one of {pack.INPUT_FORMATS}")
     u8 = input_format == "uint8_nhwc"
     src = str(onnx_file_path)
-    if precision not in ("fp16", "fp32"):
+    if precision not in pack.PRECISIONS:
         raise ValueError(f"[MDET] unknown precision {precision!r}")
-    if precision == "fp32":
-        raise NotImplementedError("[MDET] the MI355X engine computes fp16 (fp32 accumulate); "
-                                  "build with precision='fp16'")
     if dynamic_input_shapes is not None:
         mn, opt, mx = [tuple(int(v) for v in s) for s in dynamic_input_shapes[:3]]
         if not (mn[1:] == opt[1:] == mx[1:]):
@@ -248,7 +251,7 @@ def get_engine(onnx_file_path, engine_file_path="", precision="fp32", dynamic_in
         else:
             encoder = encoder or _infer_encoder(sd)
             cfg = weights.model_config(encoder, depth_type, max_depth)
-        return pack.pack_bytes(sd, cfg, *input_hw, input_format=input_format)
+        return pack.pack_bytes(sd, cfg, *input_hw, input_format=input_format, precision=precision)
 
     kw = dict(profile=profile, static_batch=1)
     if engine_file_path:

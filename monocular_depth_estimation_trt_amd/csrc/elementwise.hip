@@ -14,8 +14,9 @@ namespace mde {
 namespace {
 
 // One wave per row; PER = D/64 elements per lane, lane-strided (coalesced).
-template <int PER>
-__global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict__ x, f16* __restrict__ y,
+// XT = float (fp32 residual stream) or f16 (f16 stream); statistics in fp32.
+template <int PER, class XT>
+__global__ void __launch_bounds__(256) layernorm_kernel(const XT* __restrict__ x, f16* __restrict__ y,
                                                         const float* __restrict__ g,
                                                         const float* __restrict__ bt, int rows, float eps,
                                                         int T, int skip_cls) {
@@ -29,12 +30,12 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
     if (t == 0) return;
     orow = b * (T - 1) + t - 1;
   }
-  const float* xr = x + (size_t)row * D;
+  const XT* xr = x + (size_t)row * D;
   float v[PER];
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
-    v[i] = xr[i * 64 + lane];
+    v[i] = (float)xr[i * 64 + lane];
     s += v[i];
   }
   const float mean = wave_sum(s) * (1.0f / D);
@@ -53,6 +54,67 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict_
   }
 }
 
+// f16 residual rows: 16 lanes per row, 4 rows per wave, 16 rows per
+// workgroup; a lane owns C8/16 chunks of 8 consecutive columns (16-B loads
+// and stores, all issued before the reduction); statistics in fp32 over
+// xor-shuffles inside the 16-lane group.  D = 8 * C8, C8 % 16 == 0.
+MDE_DEV float sum16(float v) {
+  v += __shfl_xor(v, 8);
+  v += __shfl_xor(v, 4);
+  v += __shfl_xor(v, 2);
+  v += __shfl_xor(v, 1);
+  return v;
+}
+
+template <int C8>
+__global__ void __launch_bounds__(256) layernorm_h8_kernel(const f16* __restrict__ x, f16* __restrict__ y,
+                                                           const float* __restrict__ g, const float* __restrict__ bt,
+                                                           int rows, float eps, int T, int skip_cls) {
+  constexpr int D = C8 * 8, PER = C8 / 16;
+  static_assert(C8 % 16 == 0, "row width");
+  const int l16 = threadIdx.x & 15;
+  const int row = blockIdx.x * 16 + (threadIdx.x >> 4);
+  if (row >= rows) return;  // whole 16-lane groups leave together
+  int orow = row;
+  if (skip_cls) {
+    const int b = row / T, t = row - (row / T) * T;
+    if (t == 0) return;
+    orow = b * (T - 1) + t - 1;
+  }
+  const f16* xr = x + (size_t)row * D;
+  f16x8 h[PER];
+#pragma unroll
+  for (int i = 0; i < PER; ++i) h[i] = *reinterpret_cast<const f16x8*>(xr + (i * 16 + l16) * 8);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += (float)h[i][j];
+  const float mean = sum16(s) * (1.0f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < PER; ++i)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float d = (float)h[i][j] - mean;
+      q += d * d;
+    }
+  const float rstd = rsqrtf(sum16(q) * (1.0f / D) + eps);
+  f16* yr = y + (size_t)orow * D;
+#pragma unroll
+  for (int i = 0; i < PER; ++i) {
+    const int c = (i * 16 + l16) * 8;
+    const float4 g0 = *reinterpret_cast<const float4*>(g + c), g1 = *reinterpret_cast<const float4*>(g + c + 4);
+    const float4 b0 = *reinterpret_cast<const float4*>(bt + c), b1 = *reinterpret_cast<const float4*>(bt + c + 4);
+    const float gg[8] = {g0.x, g0.y, g0.z, g0.w, g1.x, g1.y, g1.z, g1.w};
+    const float bb[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+    f16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = (f16)(((float)h[i][j] - mean) * rstd * gg[j] + bb[j]);
+    *reinterpret_cast<f16x8*>(yr + c) = o;
+  }
+}
+
 #ifndef MDE_RESIZE_F16
 #define MDE_RESIZE_F16 1  // NHWC f16 resize blend in packed f16 (0: fp32 blend, A/B)
 #endif
@@ -61,7 +123,8 @@ constexpr int PK = 3 * 14 * 16;  // patch row length (K of the patch-embed GEMM)
 
 __global__ void __launch_bounds__(256) patch_prep_kernel(const float* __restrict__ img, f16* __restrict__ P,
                                                          float* __restrict__ X, const float* __restrict__ cls_pos,
-                                                         int B, int H, int W, int ph, int pw, int T, int D) {
+                                                         int B, int H, int W, int ph, int pw, int T, int D,
+                                                         f16* __restrict__ Xh) {
   const long long np = (long long)ph * pw;
   const long long nchunk = (long long)B * np * 84;  // 3 channels x 14 rows x 2 halves
   long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -92,7 +155,8 @@ __global__ void __launch_bounds__(256) patch_prep_kernel(const float* __restrict
   id -= nchunk;
   if (id < (long long)B * D) {
     const int b = (int)(id / D), d = (int)(id - (long long)(id / D) * D);
-    X[(size_t)b * T * D + d] = cls_pos[d];
+    if (Xh) Xh[(size_t)b * T * D + d] = (f16)cls_pos[d];
+    else X[(size_t)b * T * D + d] = cls_pos[d];
   }
 }
 
@@ -109,7 +173,7 @@ struct InNorm {
 __global__ void __launch_bounds__(256) patch_prep_u8_kernel(const unsigned char* __restrict__ img, f16* __restrict__ P,
                                                             float* __restrict__ X, const float* __restrict__ cls_pos,
                                                             int B, int H, int W, int ph, int pw, int T, int D,
-                                                            InNorm nrm) {
+                                                            InNorm nrm, f16* __restrict__ Xh) {
   const long long np = (long long)ph * pw;
   const long long nchunk = (long long)B * np * 28;  // 14 rows x 2 halves
   long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -139,9 +203,10 @@ __global__ void __launch_bounds__(256) patch_prep_u8_kernel(const unsigned char*
     return;
   }
   id -= nchunk;
-  if (X && id < (long long)B * D) {
+  if ((X || Xh) && id < (long long)B * D) {
     const int b = (int)(id / D), d = (int)(id - (long long)(id / D) * D);
-    X[(size_t)b * T * D + d] = cls_pos[d];
+    if (Xh) Xh[(size_t)b * T * D + d] = (f16)cls_pos[d];
+    else X[(size_t)b * T * D + d] = cls_pos[d];
   }
 }
 
@@ -239,35 +304,41 @@ __global__ void __launch_bounds__(256) resize_kernel(const f16* __restrict__ in,
 }  // namespace
 
 hipError_t launch_layernorm(const float* x, h16* y, const float* g, const float* b, int rows, int D, float eps,
-                            int T, int skip_cls, hipStream_t st) {
+                            int T, int skip_cls, hipStream_t st, const h16* xh) {
   if (rows <= 0) return hipSuccess;
   dim3 grid((rows + 3) / 4), block(256);
   f16* yo = reinterpret_cast<f16*>(y);
+  const f16* xf = reinterpret_cast<const f16*>(xh);
+#define MDE_LN(PER)                                                                                                 \
+  if (xh) hipLaunchKernelGGL((layernorm_h8_kernel<PER * 8>), dim3((rows + 15) / 16), block, 0, st, xf, yo, g, b, rows, \
+                             eps, T, skip_cls);                                                                      \
+  else hipLaunchKernelGGL((layernorm_kernel<PER, float>), grid, block, 0, st, x, yo, g, b, rows, eps, T, skip_cls);
   switch (D) {
-    case 128: hipLaunchKernelGGL(layernorm_kernel<2>, grid, block, 0, st, x, yo, g, b, rows, eps, T, skip_cls); break;
-    case 256: hipLaunchKernelGGL(layernorm_kernel<4>, grid, block, 0, st, x, yo, g, b, rows, eps, T, skip_cls); break;
-    case 384: hipLaunchKernelGGL(layernorm_kernel<6>, grid, block, 0, st, x, yo, g, b, rows, eps, T, skip_cls); break;
-    case 768: hipLaunchKernelGGL(layernorm_kernel<12>, grid, block, 0, st, x, yo, g, b, rows, eps, T, skip_cls); break;
-    case 1024: hipLaunchKernelGGL(layernorm_kernel<16>, grid, block, 0, st, x, yo, g, b, rows, eps, T, skip_cls); break;
+    case 128: MDE_LN(2) break;
+    case 256: MDE_LN(4) break;
+    case 384: MDE_LN(6) break;
+    case 768: MDE_LN(12) break;
+    case 1024: MDE_LN(16) break;
     default: return hipErrorInvalidValue;
   }
+#undef MDE_LN
   return hipGetLastError();
 }
 
 hipError_t launch_patch_prep(const float* img, h16* P, float* X, const float* cls_pos, int B, int H, int W, int ph,
-                             int pw, int T, int D, hipStream_t st) {
+                             int pw, int T, int D, hipStream_t st, h16* Xh) {
   const long long n = (long long)B * ph * pw * 84 + (long long)B * D;
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(patch_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, img,
-                     reinterpret_cast<f16*>(P), X, cls_pos, B, H, W, ph, pw, T, D);
+                     reinterpret_cast<f16*>(P), X, cls_pos, B, H, W, ph, pw, T, D, reinterpret_cast<f16*>(Xh));
   return hipGetLastError();
 }
 
 hipError_t launch_patch_prep_u8(const unsigned char* img, h16* P, float* X, const float* cls_pos, int B, int H, int W,
                                 int ph, int pw, int T, int D, float scale, const float* mean3, const float* std3,
-                                hipStream_t st) {
+                                hipStream_t st, h16* Xh) {
   if (ph < 1 || pw < 1 || H < ph * 14 || W < pw * 14 || scale == 0.f) return hipErrorInvalidValue;
-  const long long n = (long long)B * ph * pw * 28 + (X ? (long long)B * D : 0);
+  const long long n = (long long)B * ph * pw * 28 + ((X || Xh) ? (long long)B * D : 0);
   if (n <= 0) return hipSuccess;
   InNorm nrm;
   nrm.scale = scale;
@@ -276,7 +347,7 @@ hipError_t launch_patch_prep_u8(const unsigned char* img, h16* P, float* X, cons
     nrm.stdv[c] = std3[c];
   }
   hipLaunchKernelGGL(patch_prep_u8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, img,
-                     reinterpret_cast<f16*>(P), X, cls_pos, B, H, W, ph, pw, T, D, nrm);
+                     reinterpret_cast<f16*>(P), X, cls_pos, B, H, W, ph, pw, T, D, nrm, reinterpret_cast<f16*>(Xh));
   return hipGetLastError();
 }
 
@@ -293,7 +364,8 @@ namespace {
 // second half of the E_RESID split-K path (gemm.hip): one thread per 4
 // columns, slices added in order 0..S-1, then the E_RESID update
 __global__ void splitk_resid_kernel(const float* __restrict__ P, int S, int M, int N, const float* __restrict__ bias,
-                                    const float* __restrict__ ls, float* __restrict__ x32, int ldo) {
+                                    const float* __restrict__ ls, float* __restrict__ x32, f16* __restrict__ xh,
+                                    int ldo) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int n4 = N >> 2;
   if (i >= (long long)M * n4) return;
@@ -306,6 +378,16 @@ __global__ void splitk_resid_kernel(const float* __restrict__ P, int S, int M, i
   }
   const float4 bn = bias ? *reinterpret_cast<const float4*>(bias + n) : float4{0.f, 0.f, 0.f, 0.f};
   const float4 l = *reinterpret_cast<const float4*>(ls + n);
+  if (xh) {
+    f16x4* x = reinterpret_cast<f16x4*>(xh + (size_t)m * ldo + n);
+    f16x4 xv = *x;
+    xv[0] = (f16)((float)xv[0] + l.x * (a.x + bn.x));
+    xv[1] = (f16)((float)xv[1] + l.y * (a.y + bn.y));
+    xv[2] = (f16)((float)xv[2] + l.z * (a.z + bn.z));
+    xv[3] = (f16)((float)xv[3] + l.w * (a.w + bn.w));
+    *x = xv;
+    return;
+  }
   float4* x = reinterpret_cast<float4*>(x32 + (size_t)m * ldo + n);
   float4 xv = *x;
   xv.x += l.x * (a.x + bn.x);
@@ -317,12 +399,12 @@ __global__ void splitk_resid_kernel(const float* __restrict__ P, int S, int M, i
 }  // namespace
 
 hipError_t launch_splitk_resid(const float* P, int S, int M, int N, const float* bias, const float* ls, float* x32,
-                               int ldo, hipStream_t st) {
+                               h16* xh, int ldo, hipStream_t st) {
   if (S < 1 || (N & 3) || (ldo & 3) || !ls) return hipErrorInvalidValue;
   const long long n = (long long)M * (N >> 2);
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(splitk_resid_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P, S, M, N, bias, ls,
-                     x32, ldo);
+                     x32, reinterpret_cast<f16*>(xh), ldo);
   return hipGetLastError();
 }
 

@@ -45,6 +45,7 @@ std::string setup_dav2(mde_engine* e) {
       c.img_h <= 0 || c.img_w <= 0 || c.features % 16 || c.head_hidden != 32)
     return "unsupported model geometry in packed config";
   if (c.input_u8 != 0 && c.input_u8 != 1) return "bad input format in packed config";
+  if (c.resid_f16 != 0 && c.resid_f16 != 1) return "bad residual precision in packed config";
   if (c.input_u8 && (c.in_scale == 0.f || c.in_std[0] == 0.f || c.in_std[1] == 0.f || c.in_std[2] == 0.f))
     return "uint8 input preamble with a zero scale/std";
   e->D = c.embed_dim;
@@ -165,7 +166,16 @@ size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
   const size_t s0 = (size_t)(8 * e.ph) * (8 * e.pw);
   DAV2Buf t{};
   t.P = a.h(bb * np * 672);
-  t.X = a.f(bb * e.T * D);
+  // residual stream in f16 (precision "fp16": the fp32 update rounded once
+  // per residual add, as an fp16 TensorRT engine computes it -- half the
+  // bytes of every residual read-modify-write and LayerNorm read) or fp32
+  if (e.cfg.resid_f16) {
+    t.X = nullptr;
+    t.Xh = a.h(bb * e.T * D);
+  } else {
+    t.X = a.f(bb * e.T * D);
+    t.Xh = nullptr;
+  }
   t.Hn = a.h(bb * e.T * D);
   t.Q = a.h(bb * e.H * e.Tpad * 64);
   t.K = a.h(bb * e.H * e.Tpad * 64);
@@ -187,7 +197,6 @@ size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
   t.p3 = a.h(bb * s2 * F);
   t.p2 = a.h(bb * s1 * F);
   t.c1 = a.h(bb * s0 * (F / 2));
-  t.lncnt = (unsigned*)a.take((bb * e.T / 32 + 1) * 4);  // >= one word per 32-row block
   t.ws = bb * e.T <= 4096 ? a.f(4 * bb * e.T * D) : nullptr;
   // attention split-KV workspace for the batches whose (head, 128-query)
   // grid is under one workgroup per CU (launch_attention splits those)
@@ -206,19 +215,6 @@ size_t plan_arena(const mde_engine& e, int B, mde_context* c, uint8_t* base) {
   if (e.family == FAMILY_DEPTH_PRO) return plan_arena_dp(e, B, c ? &c->d : nullptr, base);
   if (e.family == FAMILY_VGGT) return plan_arena_vggt(e, B, c ? &c->v : nullptr, base);
   return plan_arena_dav2(e, B, c ? &c->b : nullptr, base);
-}
-
-// MDE_FUSE_LN=1 folds the LayerNorms into the proj/fc2 epilogues (row-block
-// arrival counter + agent-scope release/acquire).  Opt-in: measured slower
-// on MI355X (r01: proj 54 -> 113 us, fc2 98 -> 156 us at B=32) because every
-// agent-scope release/acquire writes back / invalidates the XCD's whole L2,
-// evicting the operand tiles of the other workgroups on that XCD.
-bool fuse_ln_enabled() {
-  static const int v = [] {
-    const char* e = getenv("MDE_FUSE_LN");
-    return (e && e[0] == '1') ? 1 : 0;
-  }();
-  return v != 0;
 }
 
 }  // namespace
@@ -256,16 +252,17 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
 
   step("patch_prep", [&] {
     if (cf.input_u8)
-      return launch_patch_prep_u8((const unsigned char*)img, b.P, b.X, w32("pos.cls"), B, cf.img_h, cf.img_w, e.ph,
-                                  e.pw, T, D, cf.in_scale, cf.in_mean, cf.in_std, st);
+      return launch_patch_prep_u8((const unsigned char*)img, b.P, b.Xh ? nullptr : b.X, w32("pos.cls"), B, cf.img_h,
+                                  cf.img_w, e.ph, e.pw, T, D, cf.in_scale, cf.in_mean, cf.in_std, st, b.Xh);
     return launch_patch_prep((const float*)img, b.P, b.X, w32("pos.cls"), B, cf.img_h, cf.img_w, e.ph, e.pw, T, D,
-                             st);
+                             st, b.Xh);
   });
   {
     GemmParams g = dense(b.P, 672, "patch.w", B * np, D, 672);
     g.emode = E_PATCH;
     g.bias = w32("patch.b");
     g.x32 = b.X;
+    g.xh = b.Xh;
     g.ldo = D;
     g.T = T;
     g.pos = w32("pos.patch");
@@ -274,26 +271,6 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
   }
   int tap = 0;
   char nm[64];
-  const bool fuse = fuse_ln_enabled() && (D == 384 || D == 768 || D == 1024);
-  // fused LayerNorm in a residual GEMM's tail: out1 = LN(g1,b1) (token
-  // layout), out2 = final norm into a tap map (cls dropped)
-  auto fuse_ln = [&](GemmParams& g, const char* g1, const char* b1, h16* tapdst) {
-    if (!fuse) return;
-    g.ln_counter = b.lncnt;
-    g.ln_eps = cf.ln_eps;
-    g.ln_T = T;
-    if (g1) {
-      g.ln1_g = w32(g1);
-      g.ln1_b = w32(b1);
-      g.ln1_out = b.Hn;
-    }
-    if (tapdst) {
-      g.ln2_g = w32("norm.g");
-      g.ln2_b = w32("norm.b");
-      g.ln2_out = tapdst;
-      g.ln2_skip = 1;
-    }
-  };
   for (int i = 0; i < cf.depth; ++i) {
     const std::string p = "b" + std::to_string(i) + ".";
     const std::string pn = "b" + std::to_string(i + 1) + ".";
@@ -304,17 +281,15 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
     auto split_k = [&](GemmParams& g, int K) {
       const long long t64 = (long long)((B * T + 63) / 64) * ((D + 63) / 64);
       const char* sk = getenv("MDE_SPLITK");
-      if (b.ws && !g.ln_counter && t64 < 512 && K >= 1024 && !(sk && sk[0] == '0')) {
+      if (b.ws && t64 < 512 && K >= 1024 && !(sk && sk[0] == '0')) {
         g.partial = b.ws;
         g.splitk = t64 < 256 ? 4 : 2;
       }
     };
-    if (!fuse || i == 0) {
-      snprintf(nm, sizeof nm, "block%d.norm1", i);
-      step(nm, [&] {
-        return launch_layernorm(b.X, b.Hn, w32(p + "ln1.g"), w32(p + "ln1.b"), B * T, D, cf.ln_eps, T, 0, st);
-      });
-    }
+    snprintf(nm, sizeof nm, "block%d.norm1", i);
+    step(nm, [&] {
+      return launch_layernorm(b.X, b.Hn, w32(p + "ln1.g"), w32(p + "ln1.b"), B * T, D, cf.ln_eps, T, 0, st, b.Xh);
+    });
     {
       GemmParams g = dense(b.Hn, D, p + "qkv.w", B * T, 3 * D, D);
       g.emode = E_QKV;
@@ -337,18 +312,15 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
       g.bias = w32(p + "proj.b");
       g.ls = w32(p + "ls1");
       g.x32 = b.X;
+      g.xh = b.Xh;
       g.ldo = D;
-      const std::string lg = p + "ln2.g", lb = p + "ln2.b";
-      fuse_ln(g, lg.c_str(), lb.c_str(), nullptr);
       snprintf(nm, sizeof nm, "block%d.proj", i);
       gemm(nm, g);
     }
-    if (!fuse) {
-      snprintf(nm, sizeof nm, "block%d.norm2", i);
-      step(nm, [&] {
-        return launch_layernorm(b.X, b.Hn, w32(p + "ln2.g"), w32(p + "ln2.b"), B * T, D, cf.ln_eps, T, 0, st);
-      });
-    }
+    snprintf(nm, sizeof nm, "block%d.norm2", i);
+    step(nm, [&] {
+      return launch_layernorm(b.X, b.Hn, w32(p + "ln2.g"), w32(p + "ln2.b"), B * T, D, cf.ln_eps, T, 0, st, b.Xh);
+    });
     {
       GemmParams g = dense(b.Hn, D, p + "fc1.w", B * T, cf.mlp_hidden, D);
       g.emode = E_STORE;
@@ -365,21 +337,17 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
       g.bias = w32(p + "fc2.b");
       g.ls = w32(p + "ls2");
       g.x32 = b.X;
+      g.xh = b.Xh;
       g.ldo = D;
-      const bool tapped = tap < 4 && cf.taps[tap] == i;
-      const std::string lg = pn + "ln1.g", lb = pn + "ln1.b";
-      fuse_ln(g, i + 1 < cf.depth ? lg.c_str() : nullptr, lb.c_str(), tapped ? b.tap[tap] : nullptr);
       split_k(g, cf.mlp_hidden);
       snprintf(nm, sizeof nm, "block%d.fc2", i);
       gemm(nm, g);
     }
-    if (fuse && tap < 4 && cf.taps[tap] == i) {
-      ++tap;
-    } else if (tap < 4 && cf.taps[tap] == i) {
+    if (tap < 4 && cf.taps[tap] == i) {
       snprintf(nm, sizeof nm, "tap%d.norm", tap);
       h16* dst = b.tap[tap];
       step(nm, [&] {
-        return launch_layernorm(b.X, dst, w32("norm.g"), w32("norm.b"), B * T, D, cf.ln_eps, T, 1, st);
+        return launch_layernorm(b.X, dst, w32("norm.g"), w32("norm.b"), B * T, D, cf.ln_eps, T, 1, st, b.Xh);
       });
       ++tap;
     }
@@ -1060,6 +1028,15 @@ int mde_op_tap_concat_ln(const float* xa, const float* xb, int nseq, int tokens,
   if (!xa || !xb || !g || !b || !out || nseq < 0) return fail(MDE_ERR_ARG, "null argument");
   OP_RET(launch_tap_concat_ln(xa, xb, (h16*)out, g, b, nseq, tokens, npre, dim, eps, (hipStream_t)st),
          "tap_concat_ln");
+}
+
+int mde_op_layernorm_f16(const void* x, void* y, const float* g, const float* b, int rows, int dim, float eps,
+                         int tokens, int skip_cls, void* st) {
+  if (!x || !y || !g || !b) return fail(MDE_ERR_ARG, "null argument");
+  if (skip_cls && tokens < 2) return fail(MDE_ERR_ARG, "skip_cls needs tokens >= 2");
+  OP_RET(launch_layernorm(nullptr, (h16*)y, g, b, rows, dim, eps, tokens > 0 ? tokens : 1, skip_cls, (hipStream_t)st,
+                          (const h16*)x),
+         "layernorm_f16");
 }
 
 int mde_op_layernorm(const float* x, void* y, const float* g, const float* b, int rows, int dim, float eps,

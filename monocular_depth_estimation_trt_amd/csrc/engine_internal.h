@@ -30,10 +30,10 @@ inline size_t align_up(size_t v, size_t a) { return (v + a - 1) / a * a; }
 // Depth Anything V2 activations (engine.hip plan_arena_dav2)
 struct DAV2Buf {
   h16 *P, *Hn, *Q, *K, *Vt, *O, *Mh;
-  float* X;
+  float* X;   // fp32 residual stream [B*T][D] (null when Xh is used)
+  h16* Xh;    // f16 residual stream (packed precision "fp16", cfg.resid_f16), else null
   h16 *tap[4], *pj[4], *l1, *l2, *l4, *rn[4];
   h16 *tb, *sb, *ub, *vb, *p4, *p3, *p2, *c1;
-  unsigned* lncnt;  // fused-LayerNorm row-block arrival counters (zeroed, self-resetting)
   float* ws;        // fc2 split-K partials [4][B*T][D] (small-batch contexts only, else null)
   float* aws;       // attention split-KV partials (batches whose grid splits, else null)
   size_t aws_bytes;

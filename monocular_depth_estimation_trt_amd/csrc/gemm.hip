@@ -87,108 +87,6 @@ struct KGeo {
   }
 };
 
-// LayerNorm of complete rows [m0, m0+rows) of p.x32 (width D = 64*P4) into
-// the f16 outputs of p.ln1_* / p.ln2_*.  16 lanes per row (float4 loads,
-// 8-byte stores), 4 rows per wave per group, GF groups' loads in flight so
-// the tail is not a chain of dependent L2 round trips.  fp32 two-pass stats.
-MDE_DEV float sum16(float v) {
-  v += __shfl_xor(v, 8);
-  v += __shfl_xor(v, 4);
-  v += __shfl_xor(v, 2);
-  v += __shfl_xor(v, 1);
-  return v;
-}
-
-template <int NW, int P4>
-MDE_DEV void ln_rows(const GemmParams& p, int m0, int rows, int wave, int lane) {
-  constexpr int D = 64 * P4, GF = P4 <= 6 ? 4 : (P4 <= 12 ? 2 : 1);
-  const int l16 = lane & 15, sub = lane >> 4;
-  for (int r0 = wave * 4; r0 < rows; r0 += NW * 4 * GF) {
-    float4 v[GF][P4];
-#pragma unroll
-    for (int g = 0; g < GF; ++g) {
-      const int r = r0 + g * NW * 4 + sub;
-      if (r < rows) {
-        const float4* xr = reinterpret_cast<const float4*>(p.x32 + (size_t)(m0 + r) * D);
-#pragma unroll
-        for (int j = 0; j < P4; ++j) v[g][j] = xr[j * 16 + l16];
-      }
-    }
-#pragma unroll
-    for (int g = 0; g < GF; ++g) {
-      const int r = r0 + g * NW * 4 + sub;
-      float s = 0.f;
-#pragma unroll
-      for (int j = 0; j < P4; ++j) s += (v[g][j].x + v[g][j].y) + (v[g][j].z + v[g][j].w);
-      const float mean = sum16(s) * (1.f / D);
-      float q = 0.f;
-#pragma unroll
-      for (int j = 0; j < P4; ++j) {
-        v[g][j].x -= mean; v[g][j].y -= mean; v[g][j].z -= mean; v[g][j].w -= mean;
-        q += (v[g][j].x * v[g][j].x + v[g][j].y * v[g][j].y) + (v[g][j].z * v[g][j].z + v[g][j].w * v[g][j].w);
-      }
-      const float rstd = rsqrtf(sum16(q) * (1.f / D) + p.ln_eps);
-      if (r >= rows) continue;
-      const int m = m0 + r, b = m / p.ln_T, t = m - b * p.ln_T;
-#pragma unroll
-      for (int o = 0; o < 2; ++o) {
-        h16* out = o == 0 ? p.ln1_out : p.ln2_out;
-        if (!out) continue;
-        const int skip = o == 0 ? p.ln1_skip : p.ln2_skip;
-        if (skip && t == 0) continue;
-        const int orow = skip ? b * (p.ln_T - 1) + t - 1 : m;
-        const float4* gg = reinterpret_cast<const float4*>(o == 0 ? p.ln1_g : p.ln2_g);
-        const float4* bb = reinterpret_cast<const float4*>(o == 0 ? p.ln1_b : p.ln2_b);
-        f16x4* dst = reinterpret_cast<f16x4*>(out + (size_t)orow * D);
-#pragma unroll
-        for (int j = 0; j < P4; ++j) {
-          const float4 G = gg[j * 16 + l16], Bv = bb[j * 16 + l16];
-          f16x4 h;
-          h[0] = (f16)(v[g][j].x * rstd * G.x + Bv.x);
-          h[1] = (f16)(v[g][j].y * rstd * G.y + Bv.y);
-          h[2] = (f16)(v[g][j].z * rstd * G.z + Bv.z);
-          h[3] = (f16)(v[g][j].w * rstd * G.w + Bv.w);
-          dst[j * 16 + l16] = h;
-        }
-      }
-    }
-  }
-}
-
-// Row-block completion for the fused LayerNorm: every workgroup of a row
-// block publishes its x32 tile (agent-scope release, arrival counter); the
-// last one to arrive acquires and normalises the complete rows.  Placement
-// independent; the counter is reset by the last arriver (zeroed at context
-// creation), so every launch starts from 0 (cdna_hip_programming.md G16).
-template <int NW>
-MDE_DEV void ln_tail(const GemmParams& p, int tm, int m0, int BMr, int ntn, char* smem, int tid) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  unsigned* flag = reinterpret_cast<unsigned*>(smem);
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    const unsigned old = __hip_atomic_fetch_add(p.ln_counter + tm, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    *flag = (old == (unsigned)(ntn - 1)) ? 1u : 0u;
-  }
-  __syncthreads();
-  if (*flag == 0u) return;
-  if (tid == 0) {
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __hip_atomic_store(p.ln_counter + tm, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-  __syncthreads();
-  const int rows = (p.M - m0) < BMr ? (p.M - m0) : BMr;
-  const int wave = tid >> 6, lane = tid & 63;
-  switch (p.N) {
-    case 384: ln_rows<NW, 6>(p, m0, rows, wave, lane); break;
-    case 768: ln_rows<NW, 12>(p, m0, rows, wave, lane); break;
-    case 1024: ln_rows<NW, 16>(p, m0, rows, wave, lane); break;
-    default: break;  // rejected by launch_gemm
-  }
-}
-
 template <int BM, int BN, int BK, int WM, int WN, int AM, int EM>
 __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) {
   using G = KGeo<BK>;
@@ -463,9 +361,6 @@ __global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) 
         smem + wave * (TM * 16) * (TN * 16) * 4);
   }
   if (!staged) store_tile<EM, TM, TN>(p, acc, mrow, n0 + wn * TN * 16 + (lane >> 4) * 4, lane);
-  if constexpr (EM == E_RESID) {
-    if (p.ln_counter) ln_tail<NW>(p, tm, m0, BM, ntn, smem, tid);
-  }
 }
 template <int BM, int BN, int WM, int WN, int AM, int EM>
 hipError_t run(const GemmParams& p, hipStream_t st) {
@@ -559,9 +454,8 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
   if (p.emode == E_HEAD && (p.N != 32 || p.amode == A_DENSE)) return hipErrorInvalidValue;
   if (p.amode != A_DENSE && conv_direct_supported(p) && !getenv_im2col() && !prefer_im2col(p))
     return launch_conv3(p, st);
-  if (p.ln_counter && (p.emode != E_RESID || (p.N != 384 && p.N != 768 && p.N != 1024) || p.ldo != p.N))
-    return hipErrorInvalidValue;
-  if (p.emode == E_RESID && p.splitk > 1 && p.partial && !p.ln_counter && p.amode == A_DENSE) {
+  if ((p.emode == E_RESID || p.emode == E_PATCH) && p.xh && ((uintptr_t)p.xh & 15)) return hipErrorInvalidValue;
+  if (p.emode == E_RESID && p.splitk > 1 && p.partial && p.amode == A_DENSE) {
     // small M, long K (B = 1 fc2: 132 64^2 tiles x 24 K-steps): S slices of
     // the K loop fill the chip, a second kernel adds them in slice order
     const int nk = (p.K + 63) / 64;
@@ -579,7 +473,7 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
                        dim3(256), 0, st, q);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_splitk_resid(p.partial, S, p.M, p.N, p.bias, p.ls, p.x32, p.ldo, st);
+    return launch_splitk_resid(p.partial, S, p.M, p.N, p.bias, p.ls, p.x32, p.xh, p.ldo, st);
   }
   if (gemm256_eligible(p)) return launch_gemm256(p, st);
   switch (p.amode) {

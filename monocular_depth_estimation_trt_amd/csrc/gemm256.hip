@@ -264,7 +264,7 @@ bool gemm256_eligible(const GemmParams& p) {
     const char* e = getenv("MDE_GEMM256");  // 0: never, 1: auto (default), 2: always when legal
     return e ? atoi(e) : 1;
   }();
-  if (mode == 0 || p.amode != A_DENSE || p.emode == E_HEAD || p.ln_counter) return false;
+  if (mode == 0 || p.amode != A_DENSE || p.emode == E_HEAD) return false;
   if (p.M < 256 || p.N < 256) return false;
   // short K (ViT-S: 384): the prologue/epilogue of a one-workgroup-per-CU tile
   // is not hidden behind a second workgroup -- the 128^2 kernel wins there

@@ -46,6 +46,9 @@ struct GemmParams {
   // repeated over m (row m % res0_rows: a per-image positional embedding)
   int res0_relu = 0; int res0_rows = 0;
   float* x32 = nullptr; const float* ls = nullptr;
+  // f16 residual stream: when set, E_RESID / E_PATCH update / write xh
+  // [m][ldo] f16 instead of x32 (DA-V2 engines with an f16 residual)
+  h16* xh = nullptr;
   // E_QKV
   h16 *q = nullptr, *k = nullptr, *vt = nullptr;
   int T = 0, Tpad = 0, heads = 0; float qscale = 1.0f;
@@ -59,13 +62,6 @@ struct GemmParams {
   const float* w2 = nullptr; float b2 = 0.f; int head_metric = 1; float max_depth = 1.f;
   float* out32 = nullptr;
   const h16* hpe = nullptr; int hpe_pix = 0;
-  // E_RESID + fused LayerNorm of the finished rows (ln_counter != null): the
-  // last workgroup of each row block normalises rows [m0, m0+BM) of x32 into
-  // up to two f16 outputs (gamma/beta each; skip_cls -> tap token-map layout)
-  unsigned* ln_counter = nullptr;  // one zeroed word per row block, self-resetting
-  float ln_eps = 1e-6f; int ln_T = 1;
-  const float *ln1_g = nullptr, *ln1_b = nullptr; h16* ln1_out = nullptr; int ln1_skip = 0;
-  const float *ln2_g = nullptr, *ln2_b = nullptr; h16* ln2_out = nullptr; int ln2_skip = 0;
   // E_RESID split-K (small M, long K): splitk > 1 and partial = fp32
   // workspace [splitk][M][N]; the K range is cut into splitk slices whose
   // partial sums are added in slice order by a second kernel (deterministic)
@@ -75,7 +71,7 @@ struct GemmParams {
 // x32[m*ldo+n] += ls[n] * (sum_{s<S} P[s][m][n] + bias[n]), slices summed in
 // order (elementwise.hip): the second half of the E_RESID split-K path
 hipError_t launch_splitk_resid(const float* P, int S, int M, int N, const float* bias, const float* ls, float* x32,
-                               int ldo, hipStream_t st);
+                               h16* xh, int ldo, hipStream_t st);
 
 hipError_t launch_gemm(const GemmParams& p, hipStream_t st);
 
@@ -95,16 +91,17 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
                             int Tpad, int ldo, hipStream_t st, float* ws = nullptr, size_t ws_bytes = 0);
 size_t attention_split_ws_bytes(int B, int H, int T);
 
+// x (fp32) or xh (f16) residual rows -> LayerNorm -> f16 y
 hipError_t launch_layernorm(const float* x, h16* y, const float* g, const float* b, int rows, int D,
-                            float eps, int T, int skip_cls, hipStream_t st);
+                            float eps, int T, int skip_cls, hipStream_t st, const h16* xh = nullptr);
 
 hipError_t launch_patch_prep_u8(const unsigned char* img, h16* P, float* X, const float* cls_pos, int B, int H, int W,
                                 int ph, int pw, int T, int D, float scale, const float* mean3, const float* std3,
-                                hipStream_t st);
+                                hipStream_t st, h16* Xh = nullptr);
 hipError_t launch_depth_postprocess(const float* in, int B, int ih, int iw, float* out, int oh, int ow, float lo,
                                     float hi, hipStream_t st);
 hipError_t launch_patch_prep(const float* img, h16* P, float* X, const float* cls_pos, int B, int H,
-                             int W, int ph, int pw, int T, int D, hipStream_t st);
+                             int W, int ph, int pw, int T, int D, hipStream_t st, h16* Xh = nullptr);
 
 hipError_t launch_resize(const h16* in, h16* out, int B, int ih, int iw, int C, int oh, int ow,
                          hipStream_t st);

@@ -47,7 +47,11 @@ struct PackConfig {
   // aa_depth = frame/global block pairs, agg_eps = aggregator / head LN eps
   int32_t frames, npre, aa_depth;
   float agg_eps;
-  char reserved[60];
+  // DA-V2: residual stream precision (get_engine precision): 1 = "fp16", the
+  // stream kept in f16 as an fp16 TensorRT engine computes it; 0 = "fp32",
+  // fp32 stream (Depth Pro / VGGT: always 0)
+  int32_t resid_f16;
+  char reserved[56];
 };
 static_assert(sizeof(PackConfig) == 256, "PackConfig");
 

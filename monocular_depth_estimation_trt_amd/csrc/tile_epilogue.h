@@ -125,19 +125,34 @@ MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&m
             *reinterpret_cast<f16x4*>(dst) = h;
           }
         } else if constexpr (EM == E_RESID) {
-          float4* x = reinterpret_cast<float4*>(p.x32 + (size_t)m * p.ldo + n);
           const float4 l = *reinterpret_cast<const float4*>(p.ls + n);
-          float4 xv = *x;
-          xv.x += l.x * v[0];
-          xv.y += l.y * v[1];
-          xv.z += l.z * v[2];
-          xv.w += l.w * v[3];
-          *x = xv;
+          if (p.xh) {  // f16 residual stream: fp32 update, one rounding
+            f16x4* x = reinterpret_cast<f16x4*>(reinterpret_cast<f16*>(p.xh) + (size_t)m * p.ldo + n);
+            f16x4 xv = *x;
+            xv[0] = (f16)((float)xv[0] + l.x * v[0]);
+            xv[1] = (f16)((float)xv[1] + l.y * v[1]);
+            xv[2] = (f16)((float)xv[2] + l.z * v[2]);
+            xv[3] = (f16)((float)xv[3] + l.w * v[3]);
+            *x = xv;
+          } else {
+            float4* x = reinterpret_cast<float4*>(p.x32 + (size_t)m * p.ldo + n);
+            float4 xv = *x;
+            xv.x += l.x * v[0];
+            xv.y += l.y * v[1];
+            xv.z += l.z * v[2];
+            xv.w += l.w * v[3];
+            *x = xv;
+          }
         } else if constexpr (EM == E_PATCH) {
           const int b = m / p.npatch, pi = m - (m / p.npatch) * p.npatch;
           const float4 ps = *reinterpret_cast<const float4*>(p.pos + (size_t)pi * p.ldo + n);
-          *reinterpret_cast<float4*>(p.x32 + ((size_t)b * p.T + p.tok0 + pi) * p.ldo + n) =
-              float4{v[0] + ps.x, v[1] + ps.y, v[2] + ps.z, v[3] + ps.w};
+          const size_t xo = ((size_t)b * p.T + p.tok0 + pi) * p.ldo + n;
+          if (p.xh) {
+            f16x4 h = {(f16)(v[0] + ps.x), (f16)(v[1] + ps.y), (f16)(v[2] + ps.z), (f16)(v[3] + ps.w)};
+            *reinterpret_cast<f16x4*>(reinterpret_cast<f16*>(p.xh) + xo) = h;
+          } else {
+            *reinterpret_cast<float4*>(p.x32 + xo) = float4{v[0] + ps.x, v[1] + ps.y, v[2] + ps.z, v[3] + ps.w};
+          }
         } else if constexpr (EM == E_CONVT) {
           const int q = n / p.cout, co = n - q * p.cout;
           const int dy = q / p.s, dx = q - (q / p.s) * p.s;
@@ -254,12 +269,21 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
         for (int r = 0; r < 8; ++r) h[r] = (f16)v[r];
         *reinterpret_cast<f16x8*>(reinterpret_cast<f16*>(p.out16) + o) = h;
       } else if constexpr (EM == E_RESID) {
-        float4* x = reinterpret_cast<float4*>(p.x32 + (size_t)m * p.ldo + n);
-        float4 x0 = x[0], x1 = x[1];
-        x0.x += ls0.x * v[0]; x0.y += ls0.y * v[1]; x0.z += ls0.z * v[2]; x0.w += ls0.w * v[3];
-        x1.x += ls1.x * v[4]; x1.y += ls1.y * v[5]; x1.z += ls1.z * v[6]; x1.w += ls1.w * v[7];
-        x[0] = x0;
-        x[1] = x1;
+        if (p.xh) {  // f16 residual stream: fp32 update, one rounding, 16-B RMW
+          f16x8* x = reinterpret_cast<f16x8*>(reinterpret_cast<f16*>(p.xh) + (size_t)m * p.ldo + n);
+          f16x8 xv = *x;
+          const float l8[8] = {ls0.x, ls0.y, ls0.z, ls0.w, ls1.x, ls1.y, ls1.z, ls1.w};
+#pragma unroll
+          for (int r = 0; r < 8; ++r) xv[r] = (f16)((float)xv[r] + l8[r] * v[r]);
+          *x = xv;
+        } else {
+          float4* x = reinterpret_cast<float4*>(p.x32 + (size_t)m * p.ldo + n);
+          float4 x0 = x[0], x1 = x[1];
+          x0.x += ls0.x * v[0]; x0.y += ls0.y * v[1]; x0.z += ls0.z * v[2]; x0.w += ls0.w * v[3];
+          x1.x += ls1.x * v[4]; x1.y += ls1.y * v[5]; x1.z += ls1.z * v[6]; x1.w += ls1.w * v[7];
+          x[0] = x0;
+          x[1] = x1;
+        }
       } else if constexpr (EM == E_CONVT) {
         const int q = n / p.cout, co = n - q * p.cout;
         const int dy = q / p.s, dx = q - (q / p.s) * p.s;

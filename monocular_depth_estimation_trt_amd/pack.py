@@ -178,11 +178,18 @@ IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
 
 
+PRECISIONS = ("fp16", "fp32")
+
+
 def _config_bytes(cfg: dict, img_h: int, img_w: int, input_format: str = "float32_nchw",
-                  mean=IMAGENET_MEAN, std=IMAGENET_STD, scale: float = 255.0) -> bytes:
+                  mean=IMAGENET_MEAN, std=IMAGENET_STD, scale: float = 255.0, precision: str = "fp16") -> bytes:
     """PackConfig (csrc/pack_format.h).  input_format "uint8_nhwc" stores the
     preamble constants of the reference's add_uint8_input
-    (core/onnx_tools.py:87-219): ((u8 / scale) - mean) / std, fp32."""
+    (core/onnx_tools.py:87-219): ((u8 / scale) - mean) / std, fp32.
+    precision "fp16" keeps the residual stream in f16 (resid_f16 = 1, the
+    reference's fp16 TensorRT engine), "fp32" in fp32."""
+    if precision not in PRECISIONS:
+        raise ValueError(f"precision must be one of {PRECISIONS}, got {precision!r}")
     if input_format not in INPUT_FORMATS:
         raise ValueError(f"input_format must be one of {INPUT_FORMATS}, got {input_format!r}")
     oc, taps = cfg["out_channels"], cfg["taps"]
@@ -198,7 +205,8 @@ def _config_bytes(cfg: dict, img_h: int, img_w: int, input_format: str = "float3
                      *([float(v) for v in mean] if u8 else [0.0] * 3),
                      *([float(v) for v in std] if u8 else [0.0] * 3))
     assert len(b) == 128, len(b)
-    return b + b"\0" * 128
+    b += b"\0" * 68 + struct.pack("<i", 1 if precision == "fp16" else 0)   # resid_f16 at byte 196
+    return b + b"\0" * 56
 
 
 def container(tens: "OrderedDict[str, np.ndarray]", cfg_bytes: bytes) -> bytes:
@@ -227,8 +235,9 @@ def container(tens: "OrderedDict[str, np.ndarray]", cfg_bytes: bytes) -> bytes:
 
 
 def pack_bytes(sd: Dict[str, np.ndarray], cfg: dict, img_h: int = 518, img_w: int = 518,
-               input_format: str = "float32_nchw") -> bytes:
-    return container(packed_tensors(sd, cfg, img_h, img_w), _config_bytes(cfg, img_h, img_w, input_format))
+               input_format: str = "float32_nchw", precision: str = "fp16") -> bytes:
+    return container(packed_tensors(sd, cfg, img_h, img_w),
+                     _config_bytes(cfg, img_h, img_w, input_format, precision=precision))
 
 
 def write_packed(path: str, blob: bytes) -> str:

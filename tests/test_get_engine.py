@@ -64,13 +64,25 @@ def test_errors(stub_load):
     with tempfile.TemporaryDirectory() as td:
         with pytest.raises(FileNotFoundError):
             common.get_engine(os.path.join(td, "missing.pth"), os.path.join(td, "e.mdeng"), "fp16")
-        with pytest.raises(NotImplementedError):
-            common.get_engine("synthetic:vits", os.path.join(td, "e.mdeng"), "fp32")
         with pytest.raises(ValueError):
             common.get_engine("synthetic:vits", os.path.join(td, "e.mdeng"), "int8")
         with pytest.raises(ValueError):
             common.get_engine("synthetic:vits", "", "fp16",
                               dynamic_input_shapes=[[1, 3, 70, 70], [1, 3, 84, 84], [2, 3, 70, 70]])
+
+
+def test_precision_sets_residual_stream(stub_load):
+    """precision "fp16" packs resid_f16 = 1 (f16 residual stream), "fp32" --
+    the reference's default -- packs 0 (PackConfig byte 196)."""
+    import struct
+    with tempfile.TemporaryDirectory() as td:
+        for prec, flag in (("fp16", 1), ("fp32", 0)):
+            eng = os.path.join(td, f"e_{prec}.mdeng")
+            common.get_engine("synthetic:vits", eng, prec, input_hw=(70, 70))
+            blob = open(eng, "rb").read(32 + 256)
+            assert struct.unpack_from("<i", blob, 32 + 196)[0] == flag, prec
+        common.get_engine("synthetic:vits", os.path.join(td, "d.mdeng"), input_hw=(70, 70))   # default: fp32
+        assert struct.unpack_from("<i", open(os.path.join(td, "d.mdeng"), "rb").read(288), 228)[0] == 0
 
 
 def test_staleness_rules():

@@ -181,6 +181,21 @@ def test_layernorm(gpu, D, skip):
     close(y, ref, 1e-2, 1e-2, f"layernorm D{D} skip{skip}")
 
 
+@pytest.mark.parametrize("D,skip", [(384, 0), (384, 1), (1024, 0), (768, 1), (128, 0)])
+def test_layernorm_f16_stream(gpu, D, skip):
+    """LayerNorm over the f16 residual stream of precision "fp16" engines."""
+    B, T = 3, 50
+    x = (rn(B * T, D) * 3 + 1.5).half()
+    g, b = 1 + 0.1 * rn(D), 0.02 * rn(D)
+    ref = F.layer_norm(x.float(), (D,), g, b, 1e-6)
+    if skip:
+        ref = ref.reshape(B, T, D)[:, 1:].reshape(B * (T - 1), D)
+    y = torch.empty(ref.shape, dtype=torch.float16, device=gpu)
+    op("mde_op_layernorm_f16", ptr(x.to(gpu)), ptr(y), ptr(g.to(gpu)), ptr(b.to(gpu)), B * T, D, 1e-6, T, skip,
+       stream())
+    close(y, ref, 1e-2, 1e-2, f"layernorm_f16 D{D} skip{skip}")
+
+
 @pytest.mark.parametrize("B,Hh,Ww", [(2, 98, 98), (1, 126, 182), (16, 518, 518)])
 def test_patch_embed(gpu, B, Hh, Ww):
     D = 384
