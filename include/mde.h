@@ -155,6 +155,10 @@ int mde_op_linear_residual(const void* a_f16, int lda, const void* w_f16, int ld
                            const float* bias, const float* layer_scale, float* x32, int ldx, void* stream);
 int mde_op_qkv(const void* a_f16, const void* w_f16, int ldw, const float* bias, int batch, int tokens,
                int heads, int tokens_pad, float q_scale, void* q_f16, void* k_f16, void* vt_f16, void* stream);
+/* mde_op_linear_residual over an f16 residual stream xh [m][ldx] (precision "fp16" engines):
+ * xh += layer_scale * (a W^T + bias), one rounding to f16. */
+int mde_op_linear_residual_f16(const void* a_f16, int lda, const void* w_f16, int ldw, int m, int n, int k,
+                               const float* bias, const float* layer_scale, void* xh_f16, int ldx, void* stream);
 /* q pre-multiplied by dh^-0.5 * log2(e) (scores in log2 units, as mde_op_qkv writes with
  * q_scale = 0.125 * log2(e)); k/q [B*H][tokens_pad][64], vt [B*H][64][tokens_pad] with key t
  * stored at column vt_pos(t) = t with bits 2 and 3 swapped, (t & ~12) | (t & 4) << 1 | (t & 8) >> 1

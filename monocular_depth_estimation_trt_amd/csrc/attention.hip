@@ -237,12 +237,12 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
       // P = exp2(S'), row sums, and P^T as the PV B operand: registers
       // 8s..8s+7 are k-step s (keys 16s + 8(j>>2) + 4hh + (j&3))
       f16x8 pb[2];
-      float ls0 = 0.f, ls1 = 0.f;
+      float ls0, ls1;
 #pragma unroll
       for (int r = 0; r < 16; r += 2) {
         const float p0 = __builtin_amdgcn_exp2f(sc[r]), p1 = __builtin_amdgcn_exp2f(sc[r + 1]);
-        ls0 += p0;
-        ls1 += p1;
+        ls0 = r ? ls0 + p0 : p0;
+        ls1 = r ? ls1 + p1 : p1;
         pb[r >> 3][r & 7] = (f16)p0;
         pb[r >> 3][(r & 7) + 1] = (f16)p1;
       }

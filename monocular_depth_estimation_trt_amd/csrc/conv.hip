@@ -42,6 +42,32 @@ MDE_DEV void glds16c(const void* src, void* lds_wave_base) {
 }
 MDE_DEV void wait_vmc() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
+typedef f16 f16x2c __attribute__((ext_vector_type(2)));
+
+// a + (b - a) * w on halves 2J, 2J+1: v_pk_add_f16 (neg) + v_pk_fma_f16.  The
+// subtraction is spelled out -- hipcc splits an f16x8 fsub into scalar
+// v_sub_f16 + SDWA + repack (3 VALU per pair instead of 1).  (Pairs are
+// taken with shufflevector: a bit_cast of the f16x8 to a u32x4 followed by
+// element reads miscompiles in ROCm 7.2's hipcc -- every element became
+// element 0.)
+template <int J>
+MDE_DEV f16x2c lerp2(const f16x8& a, const f16x8& b, f16x2c w2) {
+  const f16x2c a2 = __builtin_shufflevector(a, a, 2 * J, 2 * J + 1);
+  const f16x2c b2 = __builtin_shufflevector(b, b, 2 * J, 2 * J + 1);
+  unsigned dd;
+  asm("v_pk_add_f16 %0, %1, %2 neg_lo:[0,1] neg_hi:[0,1]"
+      : "=v"(dd)
+      : "v"(__builtin_bit_cast(unsigned, b2)), "v"(__builtin_bit_cast(unsigned, a2)));
+  return a2 + __builtin_bit_cast(f16x2c, dd) * w2;
+}
+
+MDE_DEV f16x8 lerp8(const f16x8& a, const f16x8& b, f16 w) {
+  const f16x2c w2 = {w, w};
+  const f16x2c r0 = lerp2<0>(a, b, w2), r1 = lerp2<1>(a, b, w2), r2 = lerp2<2>(a, b, w2), r3 = lerp2<3>(a, b, w2);
+  return __builtin_shufflevector(__builtin_shufflevector(r0, r1, 0, 1, 2, 3), __builtin_shufflevector(r2, r3, 0, 1, 2, 3),
+                                 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 template <int CK>
 MDE_DEV int cpch(int pix, int lc) {
   if constexpr (CK == 64) return lc ^ (pix & 7);
@@ -127,43 +153,50 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3_kernel(const GemmParams p)
         glds16c(src, sP + q * RWP * ROWB);
       }
     } else {
-      for (int it = tid; it < PHW * CH; it += NT) {
-        const int pp = it / CH, lc = it - (it / CH) * CH;
+      // one thread per (virtual pixel, 4 channel chunks): its source indices
+      // and weights once for 32 channels (per chunk: 3.9x the VALU at CK 32,
+      // and one item per pixel starves the 64-channel conv of lanes: output_conv1
+      // 0.205 -> 0.220 ms at B=28); 32-bit element offsets inside the image
+      // (a source map of one image is < 2^31 halves) so the four taps load
+      // as saddr + voffset; the blend on whole f16x8 vectors (lerp8)
+      const unsigned rowstride = (unsigned)p.cw * (unsigned)p.cc;
+      constexpr int CG = CH < 4 ? CH : 4, NG = CH / CG;  // chunks per item, items per pixel
+      for (int it = tid; it < PHW * NG; it += NT) {
+        const int pp = it / NG, g0 = (it - (it / NG) * NG) * CG;
         const int py = pp / PW, px = pp - (pp / PW) * PW;
         const int iy = iy0 + py, ix = ix0 + px;
-        f16x8 v = zero8();
-        if (iy >= 0 && iy < IH && ix >= 0 && ix < IW) {
-          int y0, y1, x0, x1;
-          float ly0, ly1, lx0, lx1;
+        const bool inside = iy >= 0 && iy < IH && ix >= 0 && ix < IW;
+        int y0 = 0, y1 = 0, x0 = 0, x1 = 0;
+        float ly0 = 0.f, ly1 = 0.f, lx0 = 0.f, lx1 = 0.f;
+        if (inside) {
           ac_index(usy, iy, p.ch, y0, y1, ly0, ly1);
           ac_index(usx, ix, p.cw, x0, x1, lx0, lx1);
-          const f16* base = img + cbase + lc * 8;
-          const f16x8 a = *reinterpret_cast<const f16x8*>(base + ((size_t)y0 * p.cw + x0) * p.cc);
-          const f16x8 bq = *reinterpret_cast<const f16x8*>(base + ((size_t)y0 * p.cw + x1) * p.cc);
-          const f16x8 c = *reinterpret_cast<const f16x8*>(base + ((size_t)y1 * p.cw + x0) * p.cc);
-          const f16x8 d = *reinterpret_cast<const f16x8*>(base + ((size_t)y1 * p.cw + x1) * p.cc);
-#if MDE_UP_BLEND_F16
-          // packed f16 blend in lerp form, a + (b - a) * w (v_pk_add_f16 /
-          // v_pk_fma_f16, two channels per op): the two weights of each axis
-          // sum to exactly 1, so a constant map (or a folded bias) is preserved
-          typedef f16 f16x2b __attribute__((ext_vector_type(2)));
-          const f16x2b wx1 = {(f16)lx1, (f16)lx1}, wy1 = {(f16)ly1, (f16)ly1};
+        }
+        const unsigned r0 = (unsigned)y0 * rowstride + (unsigned)cbase, r1 = (unsigned)y1 * rowstride + (unsigned)cbase;
+        const unsigned o0 = (unsigned)x0 * (unsigned)p.cc, o1 = (unsigned)x1 * (unsigned)p.cc;
 #pragma unroll
-          for (int j = 0; j < 8; j += 2) {
-            const f16x2b a2 = {a[j], a[j + 1]}, b2 = {bq[j], bq[j + 1]}, c2 = {c[j], c[j + 1]}, d2 = {d[j], d[j + 1]};
-            const f16x2b t0 = a2 + (b2 - a2) * wx1, t1 = c2 + (d2 - c2) * wx1;
-            const f16x2b r = t0 + (t1 - t0) * wy1;
-            v[j] = r[0];
-            v[j + 1] = r[1];
-          }
+        for (int q = 0; q < CG; ++q) {
+          const int lc = g0 + q;
+          f16x8 v = zero8();
+          if (inside) {
+            const f16x8 a = *reinterpret_cast<const f16x8*>(img + (r0 + o0 + lc * 8));
+            const f16x8 bq = *reinterpret_cast<const f16x8*>(img + (r0 + o1 + lc * 8));
+            const f16x8 c = *reinterpret_cast<const f16x8*>(img + (r1 + o0 + lc * 8));
+            const f16x8 d = *reinterpret_cast<const f16x8*>(img + (r1 + o1 + lc * 8));
+#if MDE_UP_BLEND_F16
+            // packed f16 blend in lerp form, a + (b - a) * w: the two weights of
+            // each axis sum to exactly 1, so a constant map (or a folded bias)
+            // is preserved
+            v = lerp8(lerp8(a, bq, (f16)lx1), lerp8(c, d, (f16)lx1), (f16)ly1);
 #else
 #pragma unroll
-          for (int j = 0; j < 8; ++j)
-            v[j] = (f16)(ly0 * (lx0 * (float)a[j] + lx1 * (float)bq[j]) + ly1 * (lx0 * (float)c[j] + lx1 * (float)d[j]));
+            for (int j = 0; j < 8; ++j)
+              v[j] = (f16)(ly0 * (lx0 * (float)a[j] + lx1 * (float)bq[j]) + ly1 * (lx0 * (float)c[j] + lx1 * (float)d[j]));
 #endif
+          }
+          if (p.relu_in) v = relu8(v);
+          *reinterpret_cast<f16x8*>(sP + pp * ROWB + cpch<CK>(pp, lc) * 16) = v;
         }
-        if (p.relu_in) v = relu8(v);
-        *reinterpret_cast<f16x8*>(sP + pp * ROWB + cpch<CK>(pp, lc) * 16) = v;
       }
     }
   };

@@ -1109,6 +1109,25 @@ int mde_op_qkv(const void* a, const void* w, int ldw, const float* bias, int bat
   OP_RET(launch_gemm(g, (hipStream_t)st), "qkv");
 }
 
+int mde_op_linear_residual_f16(const void* a, int lda, const void* w, int ldw, int m, int n, int k, const float* bias,
+                               const float* ls, void* xh, int ldx, void* st) {
+  if (!a || !w || !bias || !ls || !xh) return fail(MDE_ERR_ARG, "null argument");
+  GemmParams g;
+  g.emode = E_RESID;
+  g.A = (const h16*)a;
+  g.lda = lda;
+  g.W = (const h16*)w;
+  g.ldw = ldw;
+  g.M = m;
+  g.N = n;
+  g.K = k;
+  g.bias = bias;
+  g.ls = ls;
+  g.xh = (h16*)xh;
+  g.ldo = ldx;
+  OP_RET(launch_gemm(g, (hipStream_t)st), "linear_residual_f16");
+}
+
 int mde_op_attention(const void* q, const void* k, const void* vt, void* o, int batch, int heads, int tokens,
                      int tokens_pad, int ldo, void* st) {
   if (!q || !k || !vt || !o) return fail(MDE_ERR_ARG, "null argument");

@@ -115,6 +115,19 @@ def test_engine_vs_oracle_518_full(gpu):
     check(y, ref, 20.0, "518 B=2 vs oracle")
 
 
+def test_engine_518_b8_vs_oracle(gpu):
+    """B=8 at 518x518 (the 128^2 GEMM tiles and 8-wave attention of the
+    large-batch bench path); every image against the oracle."""
+    from oracle import dav2_ref
+    torch.set_num_threads(min(16, os.cpu_count() or 1))
+    cfg = weights.model_config("vits", "metric")
+    sd = weights.synthetic_state_dict(cfg, 4321)
+    x = weights.synthetic_images(8, 518, 518, first_seed=60)
+    ref = dav2_ref.forward(dav2_ref.to_torch(sd), cfg, x).numpy()
+    y = run_engine(pack.pack_bytes(sd, cfg, 518, 518), x)
+    check(y, ref, 20.0, "518 B=8 vs oracle")
+
+
 def test_engine_vitl_518_b2_vs_oracle(gpu):
     """ViT-L 518x518, B=2 (unsplit fc2: 688 64^2 tiles) against the oracle."""
     from oracle import dav2_ref

@@ -316,3 +316,20 @@ def test_bad_arguments_raise(gpu):
     x = torch.zeros(64, device=gpu, dtype=torch.float16)
     with pytest.raises(MDEError):  # K not a multiple of 8
         op("mde_op_linear", ptr(x), 7, ptr(x), 32, 1, 1, 7, ptr(None), 0, ptr(x), 1, stream())
+
+
+
+@pytest.mark.parametrize("m", [300, 38360])
+def test_linear_residual_f16(gpu, m):
+    """proj over the f16 residual stream of precision "fp16" engines:
+    xh += ls * (a W^T + b), fp32 update, one rounding to f16."""
+    k = n = 384
+    a, w, b = rn(m, k), rn(n, k, scale=k ** -0.5), rn(n, scale=0.1)
+    ls = 0.5 + 0.1 * rn(n)
+    x0 = (rn(m, n) * 2).half()
+    ref = x0.float() + ls * (a.half().float() @ w.half().float().T + b)
+    wp = pad_w(w).to(gpu)
+    xh = x0.to(gpu)
+    op("mde_op_linear_residual_f16", ptr(f16(a, gpu)), k, ptr(wp), wp.shape[1], m, n, k, ptr(b.to(gpu)),
+       ptr(ls.to(gpu)), ptr(xh), n, stream())
+    close(xh, ref, 1e-2, 1e-2, f"linear_residual_f16 m{m}")
