@@ -22,9 +22,10 @@ OBJDIR = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("MDE_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["gemm.hip", "conv.hip", "attention.hip", "elementwise.hip", "engine.hip",
            "depth_pro.hip", "depth_pro_ops.hip", "gemm256.hip", "vggt.hip", "vggt_ops.hip"]
-# attention: no NaN inputs by construction (masked keys are -inf, never NaN);
-# lets fmaxf lower to a bare v_max_f32 without canonicalising moves
-PER_FILE = {"attention.hip": ["-fno-honor-nans"]}
+# attention / conv: no NaN inputs by construction (masked keys are -inf, never
+# NaN; activations finite); lets fmaxf / the ReLUs lower to a bare v_max
+# without canonicalising moves (v_pk_max_f16 x, x before every f16 ReLU)
+PER_FILE = {"attention.hip": ["-fno-honor-nans"], "conv.hip": ["-fno-honor-nans"]}
 FLAGS = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
          "-Wno-unused-result", "-I", CSRC, "-I", INCLUDE]
 

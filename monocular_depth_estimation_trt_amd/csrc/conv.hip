@@ -207,6 +207,18 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3_kernel(const GemmParams p)
     for (int q = wave; q < BINS; q += NW) glds16c(wbase + (size_t)q * RWP * p.ldw + k0, dst + q * RWP * ROWB);
   };
 
+  // pre-activation ReLU of the staged (glds) patch, once per pixel in LDS
+  // instead of on each of the 9 tap reads of it; callers barrier after
+  auto relu_patch = [&] {
+    if constexpr (!UP) {
+      if (p.relu_in) {
+        for (int c = tid; c < PATCH / 16; c += NT) {
+          f16x8* q = reinterpret_cast<f16x8*>(sP + c * 16);
+          *q = relu8(*q);
+        }
+      }
+    }
+  };
   f32x4 acc[TM][TN];
 #pragma unroll
   for (int i = 0; i < TM; ++i)
@@ -221,6 +233,10 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3_kernel(const GemmParams p)
     for (int t = 0; t < 9; ++t) load_b(t, t);
     wait_vmc();
     __syncthreads();
+    if (!UP && p.relu_in) {
+      relu_patch();
+      __syncthreads();
+    }
 #pragma unroll
     for (int t = 0; t < 9; ++t) {
       const char* sB = sB0 + t * BSTAGE;
@@ -233,9 +249,6 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3_kernel(const GemmParams p)
         for (int i = 0; i < TM; ++i) {
           const int pp = ((wm * TM + i) * S + ky) * PW + (lane & 15) * S + kx;
           fa[i] = *reinterpret_cast<const f16x8*>(sP + pp * ROWB + cpch<CK>(pp, lc) * 16);
-          if constexpr (!UP) {
-            if (p.relu_in) fa[i] = relu8(fa[i]);
-          }
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -257,6 +270,10 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3_kernel(const GemmParams p)
     load_b(step0, step0 & 1);
     wait_vmc();
     __syncthreads();
+    if (!UP && p.relu_in) {
+      relu_patch();
+      __syncthreads();
+    }
     for (int t = 0; t < 9; ++t) {
       const int step = step0 + t;
       if (t + 1 < 9) load_b(step + 1, (step + 1) & 1);
@@ -271,9 +288,6 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3_kernel(const GemmParams p)
           const int py = wm * TM + i;  // tile row (TW = 16 -> one 16-row MFMA block per tile row)
           const int pp = (py * S + ky) * PW + (lane & 15) * S + kx;
           fa[i] = *reinterpret_cast<const f16x8*>(sP + pp * ROWB + cpch<CK>(pp, lc) * 16);
-          if constexpr (!UP) {
-            if (p.relu_in) fa[i] = relu8(fa[i]);
-          }
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {

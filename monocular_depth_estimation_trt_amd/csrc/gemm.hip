@@ -87,8 +87,14 @@ struct KGeo {
   }
 };
 
+#ifdef MDE_GEMM_WPE  // tuning: minimum waves per SIMD (caps VGPRs so more workgroups share a CU)
+#define MDE_GEMM_WPE_ATTR __attribute__((amdgpu_waves_per_eu(MDE_GEMM_WPE)))
+#else
+#define MDE_GEMM_WPE_ATTR
+#endif
+
 template <int BM, int BN, int BK, int WM, int WN, int AM, int EM>
-__global__ void __launch_bounds__(WM * WN * 64) gemm_kernel(const GemmParams p) {
+__global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR gemm_kernel(const GemmParams p) {
   using G = KGeo<BK>;
   constexpr int ROWB = G::ROWB, CH = G::CH;
   constexpr int NW = WM * WN;

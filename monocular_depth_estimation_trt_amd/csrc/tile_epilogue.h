@@ -200,7 +200,9 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
     int which = 0;
     if constexpr (EM == E_QKV) {
       which = n0w / (p.heads * 64);
-      if (which == 2 || (n0w & 63) + C > 64) return false;  // V^T keeps the transposing direct path
+      if ((n0w & 63) + C > 64) return false;
+      // V^T staging: one whole head, 64 token rows crossing at most one image
+      if (which == 2 && (C != 64 || R != 64 || p.T < R)) return false;
     }
     auto phys = [&](int row, int ch) { return row * (C * 4) + ((ch ^ (row & (CHR >= 8 ? 7 : CHR - 1))) << 4); };
     // ---- phase 1: accumulators (+bias, activation) -> LDS ----
@@ -228,6 +230,69 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
+    if constexpr (EM == E_QKV) {
+      if (which == 2) {
+        // ---- phase 2 for V^T [bh][64 dh][Tpad]: a lane takes a quad of 4
+        // consecutive token rows x 4 dh columns (4 conflict-free ds_read_b128:
+        // the 16 lanes of an LDS phase read 16 different chunks of the same
+        // rows), transposes it in registers and stores 4 token quads (8 B
+        // each; vt_pos keeps 4-aligned quads contiguous) -- 16 8-B stores per
+        // lane instead of 64 2-byte column stores.  Quads are aligned in token
+        // space (t % 4 == 0, one image); a quad cut by the tile edge or an
+        // image boundary stores element-wise, as do rows [0, shift).
+        // (GEMM rows are contiguous: m = m0 + r.  The tile's 64 rows cross at
+        // most one image boundary, at row rb: one division per lane.)
+        const int w = n0w - 2 * p.heads * 64;
+        const int m0 = mof(0);
+        const int b0 = m0 >= 0 ? m0 / p.T : 0;
+        const int t00 = m0 - b0 * p.T, rb = p.T - t00;  // row rb starts image b0 + 1
+        const int shift = m0 >= 0 ? (4 - t00 % 4) % 4 : 0;
+        f16* vt0 = reinterpret_cast<f16*>(p.vt) + (size_t)(w >> 6) * 64 * p.Tpad;
+        const int cc = lane & 15;  // 16-B chunk = dh 4cc .. 4cc+3
+        const size_t hs = (size_t)p.heads * 64 * p.Tpad;  // one image's V^T
+#pragma unroll
+        for (int it = 0; it < 4; ++it) {
+          const int r0 = shift + 4 * (it * 4 + (lane >> 4));
+          int mm[4], be[4], te[4];
+          f32x4 rows[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const bool in = r0 + e < R;
+            mm[e] = in ? mof(r0 + e) : -1;
+            be[e] = b0 + (r0 + e >= rb ? 1 : 0);
+            te[e] = t00 + r0 + e - (r0 + e >= rb ? p.T : 0);
+            rows[e] = in ? *reinterpret_cast<const f32x4*>(lds + phys(r0 + e, cc)) : f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+          const bool quad = mm[0] >= 0 && mm[3] >= 0 && (te[0] & 3) == 0 && be[3] == be[0];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            f16* col = vt0 + (size_t)(4 * cc + k) * p.Tpad;
+            if (quad) {
+              f16x4 h = {(f16)rows[0][k], (f16)rows[1][k], (f16)rows[2][k], (f16)rows[3][k]};
+              *reinterpret_cast<f16x4*>(col + be[0] * hs + vt_pos(te[0])) = h;
+            } else {
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                if (mm[e] >= 0) col[be[e] * hs + vt_pos(te[e])] = (f16)rows[e][k];
+            }
+          }
+        }
+        if (shift > 0) {  // rows [0, shift): lane -> (row lane >> 4, dh 16 it + lane & 15)
+          const int r = lane >> 4;
+          const int m = r < shift ? mof(r) : -1;
+          if (m >= 0) {
+            const int be = b0 + (r >= rb ? 1 : 0), te = t00 + r - (r >= rb ? p.T : 0);
+#pragma unroll
+            for (int it = 0; it < 4; ++it) {
+              const int d = it * 16 + (lane & 15);
+              const float v = *reinterpret_cast<const float*>(lds + phys(r, d >> 2) + (d & 3) * 4);
+              vt0[(size_t)d * p.Tpad + be * hs + vt_pos(te)] = (f16)v;
+            }
+          }
+        }
+        return true;
+      }
+    }
     // ---- phase 2: whole rows out ----
     const int rr = lane / CPR, cc = lane - (lane / CPR) * CPR;
     const int n = n0w + cc * 8;

@@ -63,6 +63,9 @@ def test_linear_residual(gpu, m, n, k):
 
 
 @pytest.mark.parametrize("B,T,H", [(2, 50, 6), (16, 1370, 6),
+                                   # 128^2 tiles with the LDS-staged V^T quads: image boundaries
+                                   # inside tiles at every token alignment (T % 4 = 1, 3)
+                                   (100, 37, 6), (3, 1371, 6),
                                    # D 1024, 75 x 12 tiles of 256^2 (>= 80 % of 4 rounds): gemm256 E_QKV
                                    (14, 1370, 16)])
 def test_qkv_layout(gpu, B, T, H):
