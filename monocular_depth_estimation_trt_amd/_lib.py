@@ -91,7 +91,9 @@ PROTOTYPES = {
     "mde_op_qkv": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p,
                    c_void_p, c_void_p],
     "mde_op_linear_residual_f16": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
-                                   c_void_p, c_int, c_void_p],
+                                   c_void_p, c_int, c_void_p, c_void_p],
+    "mde_op_linear_lnfold": [c_void_p, c_void_p, c_float, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                             c_int, c_void_p, c_int, c_void_p],
     "mde_op_attention_ws": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                             c_size_t, c_void_p],
     "mde_op_attention_ws_bytes": [c_int, c_int, c_int],

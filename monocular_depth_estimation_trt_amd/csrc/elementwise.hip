@@ -124,7 +124,8 @@ constexpr int PK = 3 * 14 * 16;  // patch row length (K of the patch-embed GEMM)
 __global__ void __launch_bounds__(256) patch_prep_kernel(const float* __restrict__ img, f16* __restrict__ P,
                                                          float* __restrict__ X, const float* __restrict__ cls_pos,
                                                          int B, int H, int W, int ph, int pw, int T, int D,
-                                                         f16* __restrict__ Xh) {
+                                                         f16* __restrict__ Xh, float* __restrict__ lnst,
+                                                         const float* __restrict__ cls_st) {
   const long long np = (long long)ph * pw;
   const long long nchunk = (long long)B * np * 84;  // 3 channels x 14 rows x 2 halves
   long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -157,6 +158,14 @@ __global__ void __launch_bounds__(256) patch_prep_kernel(const float* __restrict
     const int b = (int)(id / D), d = (int)(id - (long long)(id / D) * D);
     if (Xh) Xh[(size_t)b * T * D + d] = (f16)cls_pos[d];
     else X[(size_t)b * T * D + d] = cls_pos[d];
+    return;
+  }
+  id -= (long long)B * D;
+  // the cls rows' LayerNorm partials (folded LN, GemmParams::lnst_out): the
+  // row is the same f16 vector in every image, its partials come packed
+  if (lnst && id < (long long)B * (D / 16)) {
+    const int per = D / 16, b = (int)(id / per), k = (int)(id - (long long)b * per);
+    lnst[((size_t)(k >> 1) * B * T + (size_t)b * T) * 2 + (k & 1)] = cls_st[k];
   }
 }
 
@@ -173,7 +182,8 @@ struct InNorm {
 __global__ void __launch_bounds__(256) patch_prep_u8_kernel(const unsigned char* __restrict__ img, f16* __restrict__ P,
                                                             float* __restrict__ X, const float* __restrict__ cls_pos,
                                                             int B, int H, int W, int ph, int pw, int T, int D,
-                                                            InNorm nrm, f16* __restrict__ Xh) {
+                                                            InNorm nrm, f16* __restrict__ Xh, float* __restrict__ lnst,
+                                                            const float* __restrict__ cls_st) {
   const long long np = (long long)ph * pw;
   const long long nchunk = (long long)B * np * 28;  // 14 rows x 2 halves
   long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
@@ -207,6 +217,12 @@ __global__ void __launch_bounds__(256) patch_prep_u8_kernel(const unsigned char*
     const int b = (int)(id / D), d = (int)(id - (long long)(id / D) * D);
     if (Xh) Xh[(size_t)b * T * D + d] = (f16)cls_pos[d];
     else X[(size_t)b * T * D + d] = cls_pos[d];
+    return;
+  }
+  if (X || Xh) id -= (long long)B * D;
+  if (lnst && id < (long long)B * (D / 16)) {
+    const int per = D / 16, b = (int)(id / per), k = (int)(id - (long long)b * per);
+    lnst[((size_t)(k >> 1) * B * T + (size_t)b * T) * 2 + (k & 1)] = cls_st[k];
   }
 }
 
@@ -326,19 +342,23 @@ hipError_t launch_layernorm(const float* x, h16* y, const float* g, const float*
 }
 
 hipError_t launch_patch_prep(const float* img, h16* P, float* X, const float* cls_pos, int B, int H, int W, int ph,
-                             int pw, int T, int D, hipStream_t st, h16* Xh) {
-  const long long n = (long long)B * ph * pw * 84 + (long long)B * D;
+                             int pw, int T, int D, hipStream_t st, h16* Xh, float* lnst, const float* cls_st) {
+  if (lnst && (!cls_st || (D & 31))) return hipErrorInvalidValue;
+  const long long n = (long long)B * ph * pw * 84 + (long long)B * D + (lnst ? (long long)B * (D / 16) : 0);
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(patch_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, img,
-                     reinterpret_cast<f16*>(P), X, cls_pos, B, H, W, ph, pw, T, D, reinterpret_cast<f16*>(Xh));
+                     reinterpret_cast<f16*>(P), X, cls_pos, B, H, W, ph, pw, T, D, reinterpret_cast<f16*>(Xh), lnst,
+                     cls_st);
   return hipGetLastError();
 }
 
 hipError_t launch_patch_prep_u8(const unsigned char* img, h16* P, float* X, const float* cls_pos, int B, int H, int W,
                                 int ph, int pw, int T, int D, float scale, const float* mean3, const float* std3,
-                                hipStream_t st, h16* Xh) {
+                                hipStream_t st, h16* Xh, float* lnst, const float* cls_st) {
   if (ph < 1 || pw < 1 || H < ph * 14 || W < pw * 14 || scale == 0.f) return hipErrorInvalidValue;
-  const long long n = (long long)B * ph * pw * 28 + ((X || Xh) ? (long long)B * D : 0);
+  if (lnst && (!cls_st || (D & 31) || !(X || Xh))) return hipErrorInvalidValue;
+  const long long n = (long long)B * ph * pw * 28 + ((X || Xh) ? (long long)B * D : 0) +
+                      (lnst ? (long long)B * (D / 16) : 0);
   if (n <= 0) return hipSuccess;
   InNorm nrm;
   nrm.scale = scale;
@@ -347,7 +367,8 @@ hipError_t launch_patch_prep_u8(const unsigned char* img, h16* P, float* X, cons
     nrm.stdv[c] = std3[c];
   }
   hipLaunchKernelGGL(patch_prep_u8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, img,
-                     reinterpret_cast<f16*>(P), X, cls_pos, B, H, W, ph, pw, T, D, nrm, reinterpret_cast<f16*>(Xh));
+                     reinterpret_cast<f16*>(P), X, cls_pos, B, H, W, ph, pw, T, D, nrm, reinterpret_cast<f16*>(Xh),
+                     lnst, cls_st);
   return hipGetLastError();
 }
 
@@ -365,10 +386,10 @@ namespace {
 // columns, slices added in order 0..S-1, then the E_RESID update
 __global__ void splitk_resid_kernel(const float* __restrict__ P, int S, int M, int N, const float* __restrict__ bias,
                                     const float* __restrict__ ls, float* __restrict__ x32, f16* __restrict__ xh,
-                                    int ldo) {
+                                    int ldo, float* __restrict__ lnst) {
   const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const int n4 = N >> 2;
-  if (i >= (long long)M * n4) return;
+  if (i >= (long long)M * n4) return;  // M * n4 is a multiple of 8 (N % 32 == 0): 8-lane groups stay whole
   const int m = (int)(i / n4), n = (int)(i - (long long)m * n4) * 4;
   const size_t plane = (size_t)M * N;
   float4 a = *reinterpret_cast<const float4*>(P + (size_t)m * N + n);
@@ -386,6 +407,21 @@ __global__ void splitk_resid_kernel(const float* __restrict__ P, int S, int M, i
     xv[2] = (f16)((float)xv[2] + l.z * (a.z + bn.z));
     xv[3] = (f16)((float)xv[3] + l.w * (a.w + bn.w));
     *x = xv;
+    if (lnst) {  // folded LN: (sum, sum of squares) of the row's 32-column slices, 8 lanes each
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float v = (float)xv[r];
+        s1 += v;
+        s2 += v * v;
+      }
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) {
+        s1 += __shfl_xor(s1, o);
+        s2 += __shfl_xor(s2, o);
+      }
+      if ((n & 31) == 0) *reinterpret_cast<float2*>(lnst + ((size_t)(n >> 5) * M + m) * 2) = make_float2(s1, s2);
+    }
     return;
   }
   float4* x = reinterpret_cast<float4*>(x32 + (size_t)m * ldo + n);
@@ -399,12 +435,12 @@ __global__ void splitk_resid_kernel(const float* __restrict__ P, int S, int M, i
 }  // namespace
 
 hipError_t launch_splitk_resid(const float* P, int S, int M, int N, const float* bias, const float* ls, float* x32,
-                               h16* xh, int ldo, hipStream_t st) {
-  if (S < 1 || (N & 3) || (ldo & 3) || !ls) return hipErrorInvalidValue;
+                               h16* xh, int ldo, hipStream_t st, float* lnst) {
+  if (S < 1 || (N & 3) || (ldo & 3) || !ls || (lnst && (!xh || (N & 31)))) return hipErrorInvalidValue;
   const long long n = (long long)M * (N >> 2);
   if (n <= 0) return hipSuccess;
   hipLaunchKernelGGL(splitk_resid_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P, S, M, N, bias, ls,
-                     x32, reinterpret_cast<f16*>(xh), ldo);
+                     x32, reinterpret_cast<f16*>(xh), ldo, lnst);
   return hipGetLastError();
 }
 

@@ -156,6 +156,15 @@ int load_pack(const uint8_t* data, size_t n, int device, mde_engine** out) {
 namespace mde {
 
 // ---- DA-V2 activation arena ---------------------------------------------------
+// MDE_LNFOLD=0: norm1 / norm2 as LayerNorm launches + the unfolded linears (A/B, tests)
+bool lnfold_off() {
+  static const bool off = [] {
+    const char* e = getenv("MDE_LNFOLD");
+    return e && e[0] == '0';
+  }();
+  return off;
+}
+
 size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
   ArenaPlan a(base);
   const size_t bb = (size_t)B;
@@ -177,6 +186,11 @@ size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
     t.Xh = nullptr;
   }
   t.Hn = a.h(bb * e.T * D);
+  // LayerNorm folded into qkv / fc1 (packs with the folded weights): the
+  // residual writers leave per-32-column (sum, sum of squares) partials here
+  t.st = (e.cfg.resid_f16 && D % 32 == 0 && D <= 512 && e.get("pos.cls.st") && !lnfold_off())
+             ? a.f(bb * e.T * (D / 16))
+             : nullptr;
   t.Q = a.h(bb * e.H * e.Tpad * 64);
   t.K = a.h(bb * e.H * e.Tpad * 64);
   t.Vt = a.h(bb * e.H * e.Tpad * 64);
@@ -250,12 +264,15 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
   const int* oc = cf.out_channels;
   DAV2Buf& b = c.b;
 
+  const bool fold = b.st != nullptr;
+  const float* cls_st = fold ? w32("pos.cls.st") : nullptr;
   step("patch_prep", [&] {
     if (cf.input_u8)
       return launch_patch_prep_u8((const unsigned char*)img, b.P, b.Xh ? nullptr : b.X, w32("pos.cls"), B, cf.img_h,
-                                  cf.img_w, e.ph, e.pw, T, D, cf.in_scale, cf.in_mean, cf.in_std, st, b.Xh);
+                                  cf.img_w, e.ph, e.pw, T, D, cf.in_scale, cf.in_mean, cf.in_std, st, b.Xh, b.st,
+                                  cls_st);
     return launch_patch_prep((const float*)img, b.P, b.X, w32("pos.cls"), B, cf.img_h, cf.img_w, e.ph, e.pw, T, D,
-                             st, b.Xh);
+                             st, b.Xh, b.st, cls_st);
   });
   {
     GemmParams g = dense(b.P, 672, "patch.w", B * np, D, 672);
@@ -267,6 +284,11 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
     g.T = T;
     g.pos = w32("pos.patch");
     g.npatch = np;
+    if (fold) {
+      g.lnst_out = b.st;
+      g.lnst_ns = D / 32;
+      g.lnst_rows = B * T;
+    }
     gemm("patch_embed", g);
   }
   int tap = 0;
@@ -286,10 +308,27 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
         g.splitk = t64 < 256 ? 4 : 2;
       }
     };
-    snprintf(nm, sizeof nm, "block%d.norm1", i);
-    step(nm, [&] {
-      return launch_layernorm(b.X, b.Hn, w32(p + "ln1.g"), w32(p + "ln1.b"), B * T, D, cf.ln_eps, T, 0, st, b.Xh);
-    });
+    // LayerNorm folded across the GEMM boundary (packs with folded weights):
+    // the consumer reads the raw f16 residual rows with W * gamma and the
+    // producers' row partials (GemmParams::lnst_in); otherwise a LayerNorm launch
+    auto ln_fold = [&](GemmParams& g, const std::string& w) {
+      g.A = b.Xh;
+      g.lda = D;
+      g.W = w16(p + w + ".wf");
+      g.ldw = ldw(p + w + ".wf");
+      g.bias = w32(p + w + ".c2");
+      g.lnst_in = b.st;
+      g.lnc1 = w32(p + w + ".c1");
+      g.lnst_ns = D / 32;
+      g.lnst_rows = B * T;
+      g.ln_eps = cf.ln_eps;
+    };
+    if (!fold) {
+      snprintf(nm, sizeof nm, "block%d.norm1", i);
+      step(nm, [&] {
+        return launch_layernorm(b.X, b.Hn, w32(p + "ln1.g"), w32(p + "ln1.b"), B * T, D, cf.ln_eps, T, 0, st, b.Xh);
+      });
+    }
     {
       GemmParams g = dense(b.Hn, D, p + "qkv.w", B * T, 3 * D, D);
       g.emode = E_QKV;
@@ -301,6 +340,7 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
       g.Tpad = e.Tpad;
       g.heads = e.H;
       g.qscale = 0.125f * 1.4426950408889634f;  // dh^-0.5 * log2(e): scores in log2 units
+      if (fold) ln_fold(g, "qkv");
       snprintf(nm, sizeof nm, "block%d.qkv", i);
       gemm(nm, g);
     }
@@ -314,13 +354,20 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
       g.x32 = b.X;
       g.xh = b.Xh;
       g.ldo = D;
+      if (fold) {
+        g.lnst_out = b.st;
+        g.lnst_ns = D / 32;
+        g.lnst_rows = B * T;
+      }
       snprintf(nm, sizeof nm, "block%d.proj", i);
       gemm(nm, g);
     }
-    snprintf(nm, sizeof nm, "block%d.norm2", i);
-    step(nm, [&] {
-      return launch_layernorm(b.X, b.Hn, w32(p + "ln2.g"), w32(p + "ln2.b"), B * T, D, cf.ln_eps, T, 0, st, b.Xh);
-    });
+    if (!fold) {
+      snprintf(nm, sizeof nm, "block%d.norm2", i);
+      step(nm, [&] {
+        return launch_layernorm(b.X, b.Hn, w32(p + "ln2.g"), w32(p + "ln2.b"), B * T, D, cf.ln_eps, T, 0, st, b.Xh);
+      });
+    }
     {
       GemmParams g = dense(b.Hn, D, p + "fc1.w", B * T, cf.mlp_hidden, D);
       g.emode = E_STORE;
@@ -328,6 +375,7 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
       g.act = ACT_GELU;
       g.out16 = b.Mh;
       g.ldo = cf.mlp_hidden;
+      if (fold) ln_fold(g, "fc1");
       snprintf(nm, sizeof nm, "block%d.fc1", i);
       gemm(nm, g);
     }
@@ -340,6 +388,11 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
       g.xh = b.Xh;
       g.ldo = D;
       split_k(g, cf.mlp_hidden);
+      if (fold) {
+        g.lnst_out = b.st;
+        g.lnst_ns = D / 32;
+        g.lnst_rows = B * T;
+      }
       snprintf(nm, sizeof nm, "block%d.fc2", i);
       gemm(nm, g);
     }
@@ -1110,8 +1163,9 @@ int mde_op_qkv(const void* a, const void* w, int ldw, const float* bias, int bat
 }
 
 int mde_op_linear_residual_f16(const void* a, int lda, const void* w, int ldw, int m, int n, int k, const float* bias,
-                               const float* ls, void* xh, int ldx, void* st) {
+                               const float* ls, void* xh, int ldx, float* ln_partials, void* st) {
   if (!a || !w || !bias || !ls || !xh) return fail(MDE_ERR_ARG, "null argument");
+  if (ln_partials && (n & 31)) return fail(MDE_ERR_ARG, "ln_partials need n % 32 == 0");
   GemmParams g;
   g.emode = E_RESID;
   g.A = (const h16*)a;
@@ -1125,7 +1179,34 @@ int mde_op_linear_residual_f16(const void* a, int lda, const void* w, int ldw, i
   g.ls = ls;
   g.xh = (h16*)xh;
   g.ldo = ldx;
+  g.lnst_out = ln_partials;
+  g.lnst_ns = n / 32;
+  g.lnst_rows = m;
   OP_RET(launch_gemm(g, (hipStream_t)st), "linear_residual_f16");
+}
+
+int mde_op_linear_lnfold(const void* x, const float* ln_partials, float eps, const void* wg, int ldw, const float* c1,
+                         const float* c2, int m, int n, int k, int act, void* out, int ldo, void* st) {
+  if (!x || !ln_partials || !wg || !c1 || !c2 || !out) return fail(MDE_ERR_ARG, "null argument");
+  if (k & 31) return fail(MDE_ERR_ARG, "k % 32 != 0");
+  GemmParams g;
+  g.A = (const h16*)x;
+  g.lda = k;
+  g.W = (const h16*)wg;
+  g.ldw = ldw;
+  g.M = m;
+  g.N = n;
+  g.K = k;
+  g.bias = c2;
+  g.act = act;
+  g.out16 = (h16*)out;
+  g.ldo = ldo;
+  g.lnst_in = ln_partials;
+  g.lnc1 = c1;
+  g.lnst_ns = k / 32;
+  g.lnst_rows = m;
+  g.ln_eps = eps;
+  OP_RET(launch_gemm(g, (hipStream_t)st), "linear_lnfold");
 }
 
 int mde_op_attention(const void* q, const void* k, const void* vt, void* o, int batch, int heads, int tokens,

@@ -37,6 +37,7 @@ struct DAV2Buf {
   float* ws;        // fc2 split-K partials [4][B*T][D] (small-batch contexts only, else null)
   float* aws;       // attention split-KV partials (batches whose grid splits, else null)
   size_t aws_bytes;
+  float* st;        // folded-LN partials [B*T][D/32][2] (f16 residual + folded pack, else null)
 };
 
 // Depth Pro activations (depth_pro.hip plan_arena_dp).  Token buffers are

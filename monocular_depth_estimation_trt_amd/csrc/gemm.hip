@@ -309,9 +309,52 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR gemm_kernel(co
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);
     }
   };
+  // folded LayerNorm: this lane's share of its rows' partials -- the 4 lanes
+  // that share a row (lane >> 4) take slices q, q + 4, q + 8, q + 12 (<= 16
+  // slices: D <= 512) -- issued behind the prologue's stage 0 as one batch of
+  // unconditional loads (clamped addresses; a predicated load compiles to a
+  // branch with its own vmcnt(0)), summed after the batch has landed
+  float s1v[TM], s2v[TM];
+  float4 c1v[TN];  // lnc1 of this lane's columns (an epilogue load would cost every tile an L2 round trip)
+  auto ln_partial_loads = [&] {
+    if constexpr (AM == A_DENSE && (EM == E_QKV || EM == E_STORE)) {
+      if (p.lnst_in) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int n = n0 + wn * TN * 16 + j * 16 + (lane >> 4) * 4;
+          c1v[j] = *reinterpret_cast<const float4*>(p.lnc1 + (n < p.N ? n : 0));
+        }
+        const float2* st2 = reinterpret_cast<const float2*>(p.lnst_in);
+        float2 t[TM][4];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int m = m0 + wm * TM * 16 + i * 16 + (lane & 15);
+          const int mc = m < p.M ? m : p.M - 1;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int sl = (lane >> 4) + 4 * k;
+            t[i][k] = st2[(size_t)(sl < p.lnst_ns ? sl : 0) * p.lnst_rows + mc];
+          }
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const bool ok = (lane >> 4) + 4 * k < p.lnst_ns;
+            s1 += ok ? t[i][k].x : 0.f;
+            s2 += ok ? t[i][k].y : 0.f;
+          }
+          s1v[i] = s1;
+          s2v[i] = s2;
+        }
+      }
+    }
+  };
   if constexpr (SG == 2) {
     issue(0, 0);
     commit_up(0);
+    ln_partial_loads();
     wait_vm();
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
@@ -328,6 +371,7 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR gemm_kernel(co
 #pragma unroll
     for (int s = 0; s < SG - 1; ++s)
       if (s < nk) issue(s, s);
+    ln_partial_loads();
     for (int kt = 0; kt < nk; ++kt) {
       const int after = min(nk - 1 - kt, SG - 2);
       if (after >= 2) wait_vm_n<2 * NPER>();
@@ -336,6 +380,38 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR gemm_kernel(co
       lds_barrier();  // stage kt visible to all waves; stage kt-1 fully consumed
       if (kt + SG - 1 < nk) issue(kt + SG - 1, (kt + SG - 1) % SG);
       mma_stage(kt % SG);
+    }
+  }
+
+  // ---- folded LayerNorm (GemmParams::lnst_in): A held the raw f16 residual
+  // rows and W = W_ln * gamma; per row, mean and rstd from the producer's
+  // 32-column partials (fp32), then acc := rstd * acc - rstd * mean * lnc1[n]
+  // (the epilogue adds bias = b + W_ln beta).  var = E[x^2] - mean^2 in fp32,
+  // clamped at 0.
+  if constexpr (AM == A_DENSE && (EM == E_QKV || EM == E_STORE)) {
+    if (p.lnst_in) {
+      // s1v / s2v: this lane's share of the row partials, loaded with the
+      // prologue (ln_partial_loads); two xor-shuffles combine the 4 lanes
+      const float invd = 1.f / (float)(p.lnst_ns * 32);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        float s1 = s1v[i], s2 = s2v[i];
+        s1 += __shfl_xor(s1, 16);
+        s2 += __shfl_xor(s2, 16);
+        s1 += __shfl_xor(s1, 32);
+        s2 += __shfl_xor(s2, 32);
+        const float mean = s1 * invd;
+        const float rstd = rsqrtf(fmaxf(s2 * invd - mean * mean, 0.f) + p.ln_eps);
+        const float nm = -rstd * mean;
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const float4 c = c1v[j];
+          acc[i][j][0] = fmaf(rstd, acc[i][j][0], nm * c.x);
+          acc[i][j][1] = fmaf(rstd, acc[i][j][1], nm * c.y);
+          acc[i][j][2] = fmaf(rstd, acc[i][j][2], nm * c.z);
+          acc[i][j][3] = fmaf(rstd, acc[i][j][3], nm * c.w);
+        }
+      }
     }
   }
 
@@ -474,14 +550,24 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
     q.ldo = p.N;
     q.bias = nullptr;
     q.ls = nullptr;
+    q.lnst_out = nullptr;  // the reduce kernel writes the LN partials
     const unsigned tiles = (unsigned)(((p.M + 63) / 64) * ((p.N + 63) / 64));
     hipLaunchKernelGGL((gemm_kernel<64, 64, MDE_GEMM_BK, 2, 2, A_DENSE, E_PARTIAL>), dim3(tiles, (unsigned)S),
                        dim3(256), 0, st, q);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
-    return launch_splitk_resid(p.partial, S, p.M, p.N, p.bias, p.ls, p.x32, p.xh, p.ldo, st);
+    return launch_splitk_resid(p.partial, S, p.M, p.N, p.bias, p.ls, p.x32, p.xh, p.ldo, st, p.lnst_out);
   }
-  if (gemm256_eligible(p)) return launch_gemm256(p, st);
+  if (p.lnst_out || p.lnst_in) {
+    // folded LayerNorm: the 128^2 / 64^2 kernels of this file (partials per
+    // 32-column slice from the LDS-staged epilogue, the fold after the main loop)
+    if ((p.lnst_ns * 32 != (p.lnst_out ? p.N : p.K)) || (p.lnst_in && (p.lnst_ns > 16 || p.lnst_rows != p.M)) ||
+        (p.lnst_out && p.lnst_rows < (p.emode == E_PATCH ? p.M / p.npatch * p.T : p.M)) || (p.lnst_in && (!p.lnc1 || p.amode != A_DENSE)) ||
+        (p.lnst_out && !p.xh))
+      return hipErrorInvalidValue;
+  } else if (gemm256_eligible(p)) {
+    return launch_gemm256(p, st);
+  }
   switch (p.amode) {
     case A_DENSE:
       switch (p.emode) {

@@ -66,12 +66,23 @@ struct GemmParams {
   // workspace [splitk][M][N]; the K range is cut into splitk slices whose
   // partial sums are added in slice order by a second kernel (deterministic)
   int splitk = 1; float* partial = nullptr;
+  // LayerNorm folded across a GEMM boundary (DA-V2 f16-residual engines):
+  //  * producer (E_RESID / E_PATCH over xh, and the split-K reduce): lnst_out
+  //    = fp32 [lnst_ns][lnst_rows][2] -- per 32-column slice and token row
+  //    (slice-major: a load of 16 consecutive rows is one 128-B line), the
+  //    sum and the sum of squares of the f16 values written;
+  //  * consumer (the next qkv / fc1, A = the raw f16 residual rows, W = W * gamma,
+  //    bias = b + W beta): lnst_in = those partials, lnc1[n] = sum_k W[n][k]
+  //    -> acc := rstd_m * (acc - mean_m * lnc1[n]) before the epilogue.
+  float* lnst_out = nullptr;
+  const float* lnst_in = nullptr; const float* lnc1 = nullptr;
+  int lnst_ns = 0, lnst_rows = 0; float ln_eps = 1e-6f;
 };
 
 // x32[m*ldo+n] += ls[n] * (sum_{s<S} P[s][m][n] + bias[n]), slices summed in
 // order (elementwise.hip): the second half of the E_RESID split-K path
 hipError_t launch_splitk_resid(const float* P, int S, int M, int N, const float* bias, const float* ls, float* x32,
-                               h16* xh, int ldo, hipStream_t st);
+                               h16* xh, int ldo, hipStream_t st, float* lnst_out = nullptr);  // lnst_out rows = M
 
 hipError_t launch_gemm(const GemmParams& p, hipStream_t st);
 
@@ -97,11 +108,13 @@ hipError_t launch_layernorm(const float* x, h16* y, const float* g, const float*
 
 hipError_t launch_patch_prep_u8(const unsigned char* img, h16* P, float* X, const float* cls_pos, int B, int H, int W,
                                 int ph, int pw, int T, int D, float scale, const float* mean3, const float* std3,
-                                hipStream_t st, h16* Xh = nullptr);
+                                hipStream_t st, h16* Xh = nullptr, float* lnst = nullptr,
+                                const float* cls_st = nullptr);
 hipError_t launch_depth_postprocess(const float* in, int B, int ih, int iw, float* out, int oh, int ow, float lo,
                                     float hi, hipStream_t st);
 hipError_t launch_patch_prep(const float* img, h16* P, float* X, const float* cls_pos, int B, int H,
-                             int W, int ph, int pw, int T, int D, hipStream_t st, h16* Xh = nullptr);
+                             int W, int ph, int pw, int T, int D, hipStream_t st, h16* Xh = nullptr,
+                             float* lnst = nullptr, const float* cls_st = nullptr);
 
 hipError_t launch_resize(const h16* in, h16* out, int B, int ih, int iw, int C, int oh, int ow,
                          hipStream_t st);

@@ -189,9 +189,12 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
   constexpr int CPR = C / 8;               // lanes per row in the read-back (8 columns each)
   constexpr int RPI = 64 / CPR;            // rows per read-back instruction
   static_assert(TN >= 1 && C % 8 == 0, "tile");
-  if constexpr (EM != E_STORE && EM != E_RESID && EM != E_QKV && EM != E_CONVT) {
+  if constexpr (EM != E_STORE && EM != E_RESID && EM != E_QKV && EM != E_CONVT && EM != E_PATCH) {
     return false;
   } else {
+    if constexpr (EM == E_RESID || EM == E_PATCH) {
+      if (p.lnst_out && (C % 32)) return false;  // LN partials need whole 32-column slices per wave
+    }
     // E_CONVT: 8 consecutive columns stay inside one sub-pixel when cout % 8 == 0,
     // so each lane writes 16 B of one output pixel (the direct path writes 8 B)
     if constexpr (EM == E_CONVT) {
@@ -302,6 +305,23 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
       ls0 = *reinterpret_cast<const float4*>(p.ls + n);
       ls1 = *reinterpret_cast<const float4*>(p.ls + n + 4);
     }
+    // folded-LN partials of the f16 residual rows written here: 4 lanes (32
+    // columns) per slice, (sum, sum of squares) -> lnst_out[n / 32][m]
+    auto ln_partials = [&](int m, const f16x8& xv) {
+      float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) {
+        const float v = (float)xv[r];
+        s1 += v;
+        s2 += v * v;
+      }
+      s1 += __shfl_xor(s1, 1);
+      s2 += __shfl_xor(s2, 1);
+      s1 += __shfl_xor(s1, 2);
+      s2 += __shfl_xor(s2, 2);
+      if ((n & 31) == 0)
+        *reinterpret_cast<float2*>(p.lnst_out + ((size_t)(n >> 5) * p.lnst_rows + m) * 2) = make_float2(s1, s2);
+    };
 #pragma unroll
     for (int it = 0; it < (R + RPI - 1) / RPI; ++it) {
       const int row = it * RPI + rr;
@@ -341,6 +361,7 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
 #pragma unroll
           for (int r = 0; r < 8; ++r) xv[r] = (f16)((float)xv[r] + l8[r] * v[r]);
           *x = xv;
+          if (p.lnst_out) ln_partials(m, xv);
         } else {
           float4* x = reinterpret_cast<float4*>(p.x32 + (size_t)m * p.ldo + n);
           float4 x0 = x[0], x1 = x[1];
@@ -348,6 +369,24 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
           x1.x += ls1.x * v[4]; x1.y += ls1.y * v[5]; x1.z += ls1.z * v[6]; x1.w += ls1.w * v[7];
           x[0] = x0;
           x[1] = x1;
+        }
+      } else if constexpr (EM == E_PATCH) {
+        // patch row m = (image, patch) -> token row b*T + tok0 + patch, + pos
+        const int b = m / p.npatch, pi = m - (m / p.npatch) * p.npatch;
+        const float4 p0 = *reinterpret_cast<const float4*>(p.pos + (size_t)pi * p.ldo + n);
+        const float4 p1 = *reinterpret_cast<const float4*>(p.pos + (size_t)pi * p.ldo + n + 4);
+        const float pp[8] = {p0.x, p0.y, p0.z, p0.w, p1.x, p1.y, p1.z, p1.w};
+        const size_t row = (size_t)b * p.T + p.tok0 + pi;
+        if (p.xh) {
+          f16x8 h;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) h[r] = (f16)(v[r] + pp[r]);
+          *reinterpret_cast<f16x8*>(reinterpret_cast<f16*>(p.xh) + row * p.ldo + n) = h;
+          if (p.lnst_out) ln_partials((int)row, h);
+        } else {
+          float4* x = reinterpret_cast<float4*>(p.x32 + row * p.ldo + n);
+          x[0] = float4{v[0] + pp[0], v[1] + pp[1], v[2] + pp[2], v[3] + pp[3]};
+          x[1] = float4{v[4] + pp[4], v[5] + pp[5], v[6] + pp[6], v[7] + pp[7]};
         }
       } else if constexpr (EM == E_CONVT) {
         const int q = n / p.cout, co = n - q * p.cout;

@@ -99,8 +99,32 @@ def normalize_keys(sd: Dict[str, np.ndarray]) -> Dict[str, np.ndarray]:
     return out
 
 
-def packed_tensors(sd: Dict[str, np.ndarray], cfg: dict, img_h: int, img_w: int) -> "OrderedDict[str, np.ndarray]":
-    """The packed tensors (name -> f16/f32 numpy array) for one input size."""
+def _fold_ln(w: np.ndarray, bias: np.ndarray, g: np.ndarray, beta: np.ndarray):
+    """LayerNorm folded into the linear that follows it (the f16-residual
+    engines' norm1 -> qkv and norm2 -> fc1, engine.hip): with x the raw
+    residual row, LN(x) W^T + b = rstd * (x (W*g)^T - mean * c1) + c2, where
+    W*g scales input column k by gamma[k], c1[n] = sum_k f16(W*g)[n][k] (the
+    operand the MFMAs see) and c2 = b + f16(W) beta.  Returns the padded f16
+    W*g, c1 and c2 (fp32, sums in fp64)."""
+    w = np.asarray(w, np.float32)
+    wg = (w.astype(np.float64) * np.asarray(g, np.float64)[None, :]).astype(np.float32)
+    c1 = wg.astype(np.float16).astype(np.float64).sum(axis=1)
+    c2 = np.asarray(bias, np.float64) + w.astype(np.float16).astype(np.float64) @ np.asarray(beta, np.float64)
+    return _pad2(wg), c1.astype(np.float32), c2.astype(np.float32)
+
+
+def _slice_partials(v: np.ndarray) -> np.ndarray:
+    """Per 32-column slice, (sum, sum of squares) of the f16-rounded row v --
+    the LayerNorm partials the fold's producers write (GemmParams::lnst_out)."""
+    h = np.asarray(v, np.float32).astype(np.float16).astype(np.float64).reshape(-1, 32)
+    return np.stack([h.sum(1), (h * h).sum(1)], 1).astype(np.float32).reshape(-1)
+
+
+def packed_tensors(sd: Dict[str, np.ndarray], cfg: dict, img_h: int, img_w: int,
+                   fold_ln: bool = False) -> "OrderedDict[str, np.ndarray]":
+    """The packed tensors (name -> f16/f32 numpy array) for one input size.
+    fold_ln (precision "fp16" engines) adds the LayerNorm-folded qkv / fc1
+    weights (`*.wf`, `*.c1`, `*.c2`) and the cls row's partials (`pos.cls.st`)."""
     sd = normalize_keys(sd)
     missing = [k for k in W.expected_keys(cfg) if k not in sd and not k.endswith("mask_token")]
     if missing:
@@ -121,6 +145,8 @@ def packed_tensors(sd: Dict[str, np.ndarray], cfg: dict, img_h: int, img_w: int)
     pos = interpolate_pos_embed(sd[p + "pos_embed"], ph, pw)
     o["pos.patch"] = np.ascontiguousarray(pos[0, 1:], dtype=np.float32)
     o["pos.cls"] = f32(sd[p + "cls_token"].reshape(-1) + pos[0, 0])
+    if fold_ln and D % 32 == 0:
+        o["pos.cls.st"] = _slice_partials(o["pos.cls"])
     for i in range(cfg["depth"]):
         b = f"{p}blocks.{i}."
         q = f"b{i}."
@@ -135,6 +161,11 @@ def packed_tensors(sd: Dict[str, np.ndarray], cfg: dict, img_h: int, img_w: int)
         o[q + "ln2.b"] = f32(sd[b + "norm2.bias"])
         o[q + "fc1.w"] = _pad2(sd[b + "mlp.fc1.weight"])
         o[q + "fc1.b"] = f32(sd[b + "mlp.fc1.bias"])
+        if fold_ln:
+            o[q + "qkv.wf"], o[q + "qkv.c1"], o[q + "qkv.c2"] = _fold_ln(
+                sd[b + "attn.qkv.weight"], sd[b + "attn.qkv.bias"], sd[b + "norm1.weight"], sd[b + "norm1.bias"])
+            o[q + "fc1.wf"], o[q + "fc1.c1"], o[q + "fc1.c2"] = _fold_ln(
+                sd[b + "mlp.fc1.weight"], sd[b + "mlp.fc1.bias"], sd[b + "norm2.weight"], sd[b + "norm2.bias"])
         o[q + "fc2.w"] = _pad2(sd[b + "mlp.fc2.weight"])
         o[q + "fc2.b"] = f32(sd[b + "mlp.fc2.bias"])
         o[q + "ls2"] = f32(sd[b + "ls2.gamma"])
@@ -236,7 +267,7 @@ def container(tens: "OrderedDict[str, np.ndarray]", cfg_bytes: bytes) -> bytes:
 
 def pack_bytes(sd: Dict[str, np.ndarray], cfg: dict, img_h: int = 518, img_w: int = 518,
                input_format: str = "float32_nchw", precision: str = "fp16") -> bytes:
-    return container(packed_tensors(sd, cfg, img_h, img_w),
+    return container(packed_tensors(sd, cfg, img_h, img_w, fold_ln=precision == "fp16"),
                      _config_bytes(cfg, img_h, img_w, input_format, precision=precision))
 
 

@@ -322,17 +322,50 @@ def test_bad_arguments_raise(gpu):
 
 
 
-@pytest.mark.parametrize("m", [300, 38360])
-def test_linear_residual_f16(gpu, m):
-    """proj over the f16 residual stream of precision "fp16" engines:
-    xh += ls * (a W^T + b), fp32 update, one rounding to f16."""
-    k = n = 384
+def ln_partials_ref(xh):
+    """(sum, sum of squares) per 32-column slice and row of f16 rows, fp64,
+    slice-major [k/32][m][2] (the layout of GemmParams::lnst_*)."""
+    v = xh.double().reshape(xh.shape[0], -1, 32)
+    return torch.stack([v.sum(-1), (v * v).sum(-1)], -1).transpose(0, 1).contiguous()
+
+
+@pytest.mark.parametrize("m,n,k", [(300, 384, 384), (38360, 384, 384), (1370, 384, 1536), (2740, 1024, 1024)])
+def test_linear_residual_f16(gpu, m, n, k):
+    """proj / fc2 over the f16 residual stream of precision "fp16" engines:
+    xh += ls * (a W^T + b), fp32 update, one rounding to f16; plus the
+    folded-LayerNorm partials of the rows written (64^2 and 128^2 tiles)."""
     a, w, b = rn(m, k), rn(n, k, scale=k ** -0.5), rn(n, scale=0.1)
     ls = 0.5 + 0.1 * rn(n)
     x0 = (rn(m, n) * 2).half()
     ref = x0.float() + ls * (a.half().float() @ w.half().float().T + b)
     wp = pad_w(w).to(gpu)
     xh = x0.to(gpu)
+    part = torch.full((n // 32, m, 2), float("nan"), device=gpu)
     op("mde_op_linear_residual_f16", ptr(f16(a, gpu)), k, ptr(wp), wp.shape[1], m, n, k, ptr(b.to(gpu)),
-       ptr(ls.to(gpu)), ptr(xh), n, stream())
+       ptr(ls.to(gpu)), ptr(xh), n, ptr(part), stream())
     close(xh, ref, 1e-2, 1e-2, f"linear_residual_f16 m{m}")
+    # partials of exactly the f16 values written (fp32 sums of <= 32 terms)
+    close(part, ln_partials_ref(xh.cpu()).float(), 1e-5, 1e-3, "ln partials")
+
+
+@pytest.mark.parametrize("m,n,k,act", [(300, 1152, 384, 0), (38360, 1536, 384, 2), (1370, 2048, 512, 2),
+                                       (5, 64, 384, 0)])
+def test_linear_lnfold(gpu, m, n, k, act):
+    """LayerNorm folded into the next linear: act(LN(x) W^T + b) from the
+    raw f16 rows, W * gamma, c1, c2 and the row partials -- against the
+    reference order (LN in fp32, rounded to f16, then the linear)."""
+    x = (rn(m, k) * 2 + 0.7).half()
+    g, bt = 1 + 0.2 * rn(k), 0.05 * rn(k)
+    w, b = rn(n, k, scale=k ** -0.5), rn(n, scale=0.1)
+    ref = F.layer_norm(x.float(), (k,), g, bt, 1e-6).half().float() @ w.half().float().T + b
+    if act == 2:
+        ref = F.gelu(ref)
+    wg = (w.double() * g.double()[None, :]).float()
+    c1 = wg.half().double().sum(1).float()
+    c2 = (b.double() + w.half().double() @ bt.double()).float()
+    wgp = pad_w(wg).to(gpu)
+    part = ln_partials_ref(x).float().to(gpu)
+    out = torch.empty(m, n, dtype=torch.float16, device=gpu)
+    op("mde_op_linear_lnfold", ptr(x.to(gpu)), ptr(part), 1e-6, ptr(wgp), wgp.shape[1], ptr(c1.to(gpu)),
+       ptr(c2.to(gpu)), m, n, k, act, ptr(out), n, stream())
+    close(out, ref, 1e-2, 1.5e-2, f"linear_lnfold {m}x{n}x{k}")

@@ -124,3 +124,39 @@ def test_module_prefix_accepted(small):
     b = pack.pack_bytes(sd, cfg, 70, 70)
     assert a == b
     assert pack.fingerprint(a) == pack.fingerprint(b) != pack.fingerprint(pack.pack_bytes(sd, cfg, 84, 84))
+
+
+def test_layernorm_fold(small):
+    """precision "fp16" packs fold norm1 / norm2 into qkv / fc1: LN(x) W^T + b
+    == rstd * (x Wg^T - mean * c1) + c2 with the packed Wg (f16), c1, c2 and
+    the row statistics from the 32-column (sum, sum of squares) partials --
+    the arithmetic of the folded GEMM (gemm.hip), in float64 here."""
+    cfg, sd = small
+    o = pack.packed_tensors(sd, cfg, 98, 98, fold_ln=True)
+    D = cfg["embed_dim"]
+    x = torch.from_numpy(np.random.default_rng(0).standard_normal((5, D)).astype(np.float32) * 3 + 1)
+    x = x.half().double()
+    for blk, ln, lin, n in ((0, "norm1", "qkv", 3 * D), (3, "norm2", "fc1", cfg["mlp_hidden"])):
+        p = f"pretrained.blocks.{blk}."
+        w = sd[p + ("attn.qkv" if lin == "qkv" else "mlp.fc1") + ".weight"]
+        b = sd[p + ("attn.qkv" if lin == "qkv" else "mlp.fc1") + ".bias"]
+        g, bt = sd[p + ln + ".weight"], sd[p + ln + ".bias"]
+        ref = F.layer_norm(x, (D,), torch.from_numpy(g).double(), torch.from_numpy(bt).double(), cfg["ln_eps"])
+        ref = ref @ torch.from_numpy(w).half().double().T + torch.from_numpy(b).double()
+        wg = torch.from_numpy(o[f"b{blk}.{lin}.wf"][:n, :D].astype(np.float64))
+        c1 = torch.from_numpy(o[f"b{blk}.{lin}.c1"]).double()
+        c2 = torch.from_numpy(o[f"b{blk}.{lin}.c2"]).double()
+        part = x.reshape(5, D // 32, 32)
+        s1, s2 = part.sum(-1).sum(-1), (part * part).sum(-1).sum(-1)
+        mean = s1 / D
+        rstd = 1.0 / torch.sqrt(s2 / D - mean * mean + cfg["ln_eps"])
+        got = rstd[:, None] * (x @ wg.T - mean[:, None] * c1[None, :]) + c2[None, :]
+        # f16 rounding of W * gamma vs of W (relative 2^-11 per weight)
+        assert torch.allclose(got, ref, rtol=2e-3, atol=2e-3 * float(ref.abs().max())), (lin, (got - ref).abs().max())
+    # the cls row's partials
+    cls = torch.from_numpy(o["pos.cls"]).half().double().reshape(D // 32, 32)
+    st = torch.from_numpy(o["pos.cls.st"]).double().reshape(D // 32, 2)
+    assert torch.allclose(st[:, 0], cls.sum(-1), rtol=1e-6, atol=1e-5)
+    assert torch.allclose(st[:, 1], (cls * cls).sum(-1), rtol=1e-6, atol=1e-5)
+    # fp32-precision packs keep the unfolded layout only
+    assert "b0.qkv.wf" not in pack.packed_tensors(sd, cfg, 98, 98)
