@@ -157,15 +157,15 @@ int mde_op_qkv(const void* a_f16, const void* w_f16, int ldw, const float* bias,
                int heads, int tokens_pad, float q_scale, void* q_f16, void* k_f16, void* vt_f16, void* stream);
 /* mde_op_linear_residual over an f16 residual stream xh [m][ldx] (precision "fp16" engines):
  * xh += layer_scale * (a W^T + bias), one rounding to f16.  ln_partials (optional, n % 32 == 0):
- * fp32 [n/32][m][2] (slice-major) = per 32-column slice and row, the sum and sum of squares of the
- * f16 values written -- the producer half of the folded LayerNorm (reference: the norm1 / norm2 after every
+ * fp32 [n/32][m][2] (slice-major) = per 32-column slice and row, the sum of the f16 values written
+ * and their squared deviations from the slice mean -- the producer half of the folded LayerNorm (reference: the norm1 / norm2 after every
  * residual add of the DINOv2 blocks, upstream Block.forward). */
 int mde_op_linear_residual_f16(const void* a_f16, int lda, const void* w_f16, int ldw, int m, int n, int k,
                                const float* bias, const float* layer_scale, void* xh_f16, int ldx, float* ln_partials,
                                void* stream);
 /* The consumer half: out = act(LayerNorm(x) W^T + b) computed as act(rstd * (x Wg^T - mean * c1) + c2)
  * over the raw f16 rows x [m][k] (k % 32 == 0), with Wg = W * gamma (column k scaled by gamma[k]),
- * c1[n] = sum_k Wg[n][k], c2 = b + W beta, and mean / rstd (fp32, eps) from ln_partials [k/32][m][2] (k <= 512). */
+ * c1[n] = sum_k Wg[n][k], c2 = b + W beta, and mean / rstd (fp32, eps) from ln_partials [k/32][m][2] (k <= 1024). */
 int mde_op_linear_lnfold(const void* x_f16, const float* ln_partials, float eps, const void* wg_f16, int ldw,
                          const float* c1, const float* c2, int m, int n, int k, int act, void* out_f16, int ldo,
                          void* stream);

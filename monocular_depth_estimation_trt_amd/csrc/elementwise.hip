@@ -407,19 +407,20 @@ __global__ void splitk_resid_kernel(const float* __restrict__ P, int S, int M, i
     xv[2] = (f16)((float)xv[2] + l.z * (a.z + bn.z));
     xv[3] = (f16)((float)xv[3] + l.w * (a.w + bn.w));
     *x = xv;
-    if (lnst) {  // folded LN: (sum, sum of squares) of the row's 32-column slices, 8 lanes each
+    if (lnst) {  // folded LN: (sum, M2 about the slice mean) of the row's 32-column slices, 8 lanes each
       float s1 = 0.f, s2 = 0.f;
 #pragma unroll
+      for (int r = 0; r < 4; ++r) s1 += (float)xv[r];
+#pragma unroll
+      for (int o = 1; o < 8; o <<= 1) s1 += __shfl_xor(s1, o);
+      const float ms = s1 * (1.f / 32.f);
+#pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float v = (float)xv[r];
-        s1 += v;
-        s2 += v * v;
+        const float d = (float)xv[r] - ms;
+        s2 += d * d;
       }
 #pragma unroll
-      for (int o = 1; o < 8; o <<= 1) {
-        s1 += __shfl_xor(s1, o);
-        s2 += __shfl_xor(s2, o);
-      }
+      for (int o = 1; o < 8; o <<= 1) s2 += __shfl_xor(s2, o);
       if ((n & 31) == 0) *reinterpret_cast<float2*>(lnst + ((size_t)(n >> 5) * M + m) * 2) = make_float2(s1, s2);
     }
     return;

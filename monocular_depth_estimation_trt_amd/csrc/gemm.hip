@@ -30,6 +30,7 @@
 //    8 B (f16) / 16 B (f32) per lane straight from the accumulators.
 #include <cstdlib>
 #include <cstring>
+#include <type_traits>
 
 #include "mde_device.h"
 #include "mde_ops.h"
@@ -310,10 +311,10 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR gemm_kernel(co
     }
   };
   // folded LayerNorm: this lane's share of its rows' partials -- the 4 lanes
-  // that share a row (lane >> 4) take slices q, q + 4, q + 8, q + 12 (<= 16
-  // slices: D <= 512) -- issued behind the prologue's stage 0 as one batch of
+  // that share a row (lane >> 4) take slices q, q + 4, ... (<= 32 slices:
+  // D <= 1024) -- issued behind the prologue's stage 0 in batches of
   // unconditional loads (clamped addresses; a predicated load compiles to a
-  // branch with its own vmcnt(0)), summed after the batch has landed
+  // branch with its own vmcnt(0)), summed after each batch has landed
   float s1v[TM], s2v[TM];
   float4 c1v[TN];  // lnc1 of this lane's columns (an epilogue load would cost every tile an L2 round trip)
   auto ln_partial_loads = [&] {
@@ -325,28 +326,53 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR gemm_kernel(co
           c1v[j] = *reinterpret_cast<const float4*>(p.lnc1 + (n < p.N ? n : 0));
         }
         const float2* st2 = reinterpret_cast<const float2*>(p.lnst_in);
-        float2 t[TM][4];
+        const float invd = 1.f / (float)(p.lnst_ns * 32);
+        // <= 16 slices (D <= 512): every row at once, 4 loads per row;
+        // up to 32 (D 1024): two rows at a time, 8 loads per row
+        auto rows = [&](auto kper_tag, int i0, int ni) {
+          constexpr int KP = decltype(kper_tag)::value;
+          float2 t[4][KP];
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int m = m0 + wm * TM * 16 + i * 16 + (lane & 15);
-          const int mc = m < p.M ? m : p.M - 1;
+          for (int ii = 0; ii < 4; ++ii) {
+            if (ii >= ni) break;
+            const int m = m0 + wm * TM * 16 + (i0 + ii) * 16 + (lane & 15);
+            const int mc = m < p.M ? m : p.M - 1;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int sl = (lane >> 4) + 4 * k;
-            t[i][k] = st2[(size_t)(sl < p.lnst_ns ? sl : 0) * p.lnst_rows + mc];
+            for (int k = 0; k < KP; ++k) {
+              const int sl = (lane >> 4) + 4 * k;
+              t[ii][k] = st2[(size_t)(sl < p.lnst_ns ? sl : 0) * p.lnst_rows + mc];
+            }
           }
-        }
+          // Chan et al.'s merge of the slices' (sum, M2): the row mean
+          // first (4-lane xor-shuffle), then M2 = sum_s M2_s + 32 (mean_s -
+          // mean)^2 -- no E[x^2] - mean^2 cancellation
 #pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          float s1 = 0.f, s2 = 0.f;
+          for (int ii = 0; ii < 4; ++ii) {
+            if (ii >= ni) break;
+            float s1 = 0.f;
 #pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const bool ok = (lane >> 4) + 4 * k < p.lnst_ns;
-            s1 += ok ? t[i][k].x : 0.f;
-            s2 += ok ? t[i][k].y : 0.f;
+            for (int k = 0; k < KP; ++k) s1 += (lane >> 4) + 4 * k < p.lnst_ns ? t[ii][k].x : 0.f;
+            s1 += __shfl_xor(s1, 16);
+            s1 += __shfl_xor(s1, 32);
+            const float mean = s1 * invd;
+            float m2 = 0.f;
+#pragma unroll
+            for (int k = 0; k < KP; ++k) {
+              const float d = t[ii][k].x * (1.f / 32.f) - mean;
+              m2 += (lane >> 4) + 4 * k < p.lnst_ns ? t[ii][k].y + 32.f * d * d : 0.f;
+            }
+            m2 += __shfl_xor(m2, 16);
+            m2 += __shfl_xor(m2, 32);
+            s1v[i0 + ii] = mean;
+            s2v[i0 + ii] = m2 * invd;  // variance
           }
-          s1v[i] = s1;
-          s2v[i] = s2;
+        };
+        if (p.lnst_ns <= 16) {
+          rows(std::integral_constant<int, 4>{}, 0, TM < 4 ? TM : 4);
+          if constexpr (TM > 4) rows(std::integral_constant<int, 4>{}, 4, TM - 4);
+        } else {
+#pragma unroll
+          for (int i0 = 0; i0 < TM; i0 += 2) rows(std::integral_constant<int, 8>{}, i0, TM - i0 < 2 ? TM - i0 : 2);
         }
       }
     }
@@ -386,22 +412,16 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR gemm_kernel(co
   // ---- folded LayerNorm (GemmParams::lnst_in): A held the raw f16 residual
   // rows and W = W_ln * gamma; per row, mean and rstd from the producer's
   // 32-column partials (fp32), then acc := rstd * acc - rstd * mean * lnc1[n]
-  // (the epilogue adds bias = b + W_ln beta).  var = E[x^2] - mean^2 in fp32,
-  // clamped at 0.
+  // (the epilogue adds bias = b + W_ln beta).  mean and variance from the
+  // slices' (sum, M2) by Chan et al.'s pairwise merge, fp32.
   if constexpr (AM == A_DENSE && (EM == E_QKV || EM == E_STORE)) {
     if (p.lnst_in) {
-      // s1v / s2v: this lane's share of the row partials, loaded with the
-      // prologue (ln_partial_loads); two xor-shuffles combine the 4 lanes
-      const float invd = 1.f / (float)(p.lnst_ns * 32);
+      // s1v / s2v: the rows' mean and variance, merged in the prologue
+      // (ln_partial_loads)
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        float s1 = s1v[i], s2 = s2v[i];
-        s1 += __shfl_xor(s1, 16);
-        s2 += __shfl_xor(s2, 16);
-        s1 += __shfl_xor(s1, 32);
-        s2 += __shfl_xor(s2, 32);
-        const float mean = s1 * invd;
-        const float rstd = rsqrtf(fmaxf(s2 * invd - mean * mean, 0.f) + p.ln_eps);
+        const float mean = s1v[i];
+        const float rstd = rsqrtf(s2v[i] + p.ln_eps);
         const float nm = -rstd * mean;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -561,7 +581,7 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
   if (p.lnst_out || p.lnst_in) {
     // folded LayerNorm: the 128^2 / 64^2 kernels of this file (partials per
     // 32-column slice from the LDS-staged epilogue, the fold after the main loop)
-    if ((p.lnst_ns * 32 != (p.lnst_out ? p.N : p.K)) || (p.lnst_in && (p.lnst_ns > 16 || p.lnst_rows != p.M)) ||
+    if ((p.lnst_ns * 32 != (p.lnst_out ? p.N : p.K)) || (p.lnst_in && (p.lnst_ns > 32 || p.lnst_rows != p.M)) ||
         (p.lnst_out && p.lnst_rows < (p.emode == E_PATCH ? p.M / p.npatch * p.T : p.M)) || (p.lnst_in && (!p.lnc1 || p.amode != A_DENSE)) ||
         (p.lnst_out && !p.xh))
       return hipErrorInvalidValue;

@@ -70,7 +70,8 @@ struct GemmParams {
   //  * producer (E_RESID / E_PATCH over xh, and the split-K reduce): lnst_out
   //    = fp32 [lnst_ns][lnst_rows][2] -- per 32-column slice and token row
   //    (slice-major: a load of 16 consecutive rows is one 128-B line), the
-  //    sum and the sum of squares of the f16 values written;
+  //    sum of the f16 values written and their squared deviations from the
+  //    slice mean (M2; merged with Chan et al.'s formula, no E[x^2] - mean^2);
   //  * consumer (the next qkv / fc1, A = the raw f16 residual rows, W = W * gamma,
   //    bias = b + W beta): lnst_in = those partials, lnc1[n] = sum_k W[n][k]
   //    -> acc := rstd_m * (acc - mean_m * lnc1[n]) before the epilogue.

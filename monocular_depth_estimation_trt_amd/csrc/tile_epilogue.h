@@ -306,18 +306,22 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
       ls1 = *reinterpret_cast<const float4*>(p.ls + n + 4);
     }
     // folded-LN partials of the f16 residual rows written here: 4 lanes (32
-    // columns) per slice, (sum, sum of squares) -> lnst_out[n / 32][m]
+    // columns) per slice, (sum, sum of squared deviations from the slice
+    // mean) -> lnst_out[n / 32][m]
     auto ln_partials = [&](int m, const f16x8& xv) {
-      float s1 = 0.f, s2 = 0.f;
+      float s1 = 0.f;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) s1 += (float)xv[r];
+      s1 += __shfl_xor(s1, 1);
+      s1 += __shfl_xor(s1, 2);
+      const float ms = s1 * (1.f / 32.f);
+      float s2 = 0.f;  // M2 about the slice mean (Chan et al.'s pairwise merge downstream)
 #pragma unroll
       for (int r = 0; r < 8; ++r) {
-        const float v = (float)xv[r];
-        s1 += v;
-        s2 += v * v;
+        const float d = (float)xv[r] - ms;
+        s2 += d * d;
       }
-      s1 += __shfl_xor(s1, 1);
       s2 += __shfl_xor(s2, 1);
-      s1 += __shfl_xor(s1, 2);
       s2 += __shfl_xor(s2, 2);
       if ((n & 31) == 0)
         *reinterpret_cast<float2*>(p.lnst_out + ((size_t)(n >> 5) * p.lnst_rows + m) * 2) = make_float2(s1, s2);

@@ -114,10 +114,12 @@ def _fold_ln(w: np.ndarray, bias: np.ndarray, g: np.ndarray, beta: np.ndarray):
 
 
 def _slice_partials(v: np.ndarray) -> np.ndarray:
-    """Per 32-column slice, (sum, sum of squares) of the f16-rounded row v --
-    the LayerNorm partials the fold's producers write (GemmParams::lnst_out)."""
+    """Per 32-column slice, (sum, sum of squared deviations from the slice
+    mean) of the f16-rounded row v -- the LayerNorm partials the fold's
+    producers write (GemmParams::lnst_out)."""
     h = np.asarray(v, np.float32).astype(np.float16).astype(np.float64).reshape(-1, 32)
-    return np.stack([h.sum(1), (h * h).sum(1)], 1).astype(np.float32).reshape(-1)
+    m2 = ((h - h.mean(1, keepdims=True)) ** 2).sum(1)
+    return np.stack([h.sum(1), m2], 1).astype(np.float32).reshape(-1)
 
 
 def packed_tensors(sd: Dict[str, np.ndarray], cfg: dict, img_h: int, img_w: int,

@@ -323,10 +323,11 @@ def test_bad_arguments_raise(gpu):
 
 
 def ln_partials_ref(xh):
-    """(sum, sum of squares) per 32-column slice and row of f16 rows, fp64,
-    slice-major [k/32][m][2] (the layout of GemmParams::lnst_*)."""
+    """(sum, squared deviations from the slice mean) per 32-column slice and
+    row of f16 rows, fp64, slice-major [k/32][m][2] (GemmParams::lnst_*)."""
     v = xh.double().reshape(xh.shape[0], -1, 32)
-    return torch.stack([v.sum(-1), (v * v).sum(-1)], -1).transpose(0, 1).contiguous()
+    m2 = ((v - v.mean(-1, keepdim=True)) ** 2).sum(-1)
+    return torch.stack([v.sum(-1), m2], -1).transpose(0, 1).contiguous()
 
 
 @pytest.mark.parametrize("m,n,k", [(300, 384, 384), (38360, 384, 384), (1370, 384, 1536), (2740, 1024, 1024)])
@@ -348,7 +349,7 @@ def test_linear_residual_f16(gpu, m, n, k):
     close(part, ln_partials_ref(xh.cpu()).float(), 1e-5, 1e-3, "ln partials")
 
 
-@pytest.mark.parametrize("m,n,k,act", [(300, 1152, 384, 0), (38360, 1536, 384, 2), (1370, 2048, 512, 2),
+@pytest.mark.parametrize("m,n,k,act", [(300, 1152, 384, 0), (38360, 1536, 384, 2), (1370, 2048, 512, 2), (1370, 3072, 1024, 2), (10960, 4096, 1024, 2),
                                        (5, 64, 384, 0)])
 def test_linear_lnfold(gpu, m, n, k, act):
     """LayerNorm folded into the next linear: act(LN(x) W^T + b) from the

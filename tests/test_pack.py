@@ -147,9 +147,11 @@ def test_layernorm_fold(small):
         c1 = torch.from_numpy(o[f"b{blk}.{lin}.c1"]).double()
         c2 = torch.from_numpy(o[f"b{blk}.{lin}.c2"]).double()
         part = x.reshape(5, D // 32, 32)
-        s1, s2 = part.sum(-1).sum(-1), (part * part).sum(-1).sum(-1)
-        mean = s1 / D
-        rstd = 1.0 / torch.sqrt(s2 / D - mean * mean + cfg["ln_eps"])
+        mean = part.sum(-1).sum(-1) / D
+        # Chan et al.'s merge of the slices' (sum, M2), as the GEMM prologue
+        ms = part.mean(-1)
+        m2 = ((part - ms[..., None]) ** 2).sum(-1) + 32 * (ms - mean[:, None]) ** 2
+        rstd = 1.0 / torch.sqrt(m2.sum(-1) / D + cfg["ln_eps"])
         got = rstd[:, None] * (x @ wg.T - mean[:, None] * c1[None, :]) + c2[None, :]
         # f16 rounding of W * gamma vs of W (relative 2^-11 per weight)
         assert torch.allclose(got, ref, rtol=2e-3, atol=2e-3 * float(ref.abs().max())), (lin, (got - ref).abs().max())
@@ -157,6 +159,6 @@ def test_layernorm_fold(small):
     cls = torch.from_numpy(o["pos.cls"]).half().double().reshape(D // 32, 32)
     st = torch.from_numpy(o["pos.cls.st"]).double().reshape(D // 32, 2)
     assert torch.allclose(st[:, 0], cls.sum(-1), rtol=1e-6, atol=1e-5)
-    assert torch.allclose(st[:, 1], (cls * cls).sum(-1), rtol=1e-6, atol=1e-5)
+    assert torch.allclose(st[:, 1], ((cls - cls.mean(-1, keepdim=True)) ** 2).sum(-1), rtol=1e-6, atol=1e-5)
     # fp32-precision packs keep the unfolded layout only
     assert "b0.qkv.wf" not in pack.packed_tensors(sd, cfg, 98, 98)
