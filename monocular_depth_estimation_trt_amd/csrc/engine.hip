@@ -188,7 +188,7 @@ size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
   t.Hn = a.h(bb * e.T * D);
   // LayerNorm folded into qkv / fc1 (packs with the folded weights): the
   // residual writers leave per-32-column (sum, sum of squares) partials here
-  t.st = (e.cfg.resid_f16 && D % 32 == 0 && D <= 1024 && e.get("pos.cls.st") && !lnfold_off())
+  t.st = (e.cfg.resid_f16 && D % 128 == 0 && D <= 1024 && e.get("pos.cls.st") && !lnfold_off())
              ? a.f(bb * e.T * (D / 16))
              : nullptr;
   t.Q = a.h(bb * e.H * e.Tpad * 64);

@@ -115,7 +115,10 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR gemm_kernel(co
   constexpr int SG = (AM == A_DENSE && AINS % NW == 0 && BINS % NW == 0 && SGMAX > 2) ? SGMAX : 2;
   constexpr int NPER = APASS + BPASS;
   static_assert(SG >= 2 && SG <= 4, "stages");
-  __shared__ __attribute__((aligned(16))) char smem[SG * STAGE];
+  // folded LayerNorm consumers: (mean, var) of the tile's rows behind the ring
+  constexpr bool LNF = AM == A_DENSE && (EM == E_QKV || EM == E_STORE);
+  constexpr int LNB = LNF ? BM * 8 : 0;
+  __shared__ __attribute__((aligned(16))) char smem[SG * STAGE + LNB];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -310,16 +313,26 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR gemm_kernel(co
         for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);
     }
   };
-  // folded LayerNorm: this lane's share of its rows' partials -- the 4 lanes
-  // that share a row (lane >> 4) take slices q, q + 4, ... (<= 32 slices:
-  // D <= 1024) -- issued behind the prologue's stage 0 in batches of
-  // unconditional loads (clamped addresses; a predicated load compiles to a
-  // branch with its own vmcnt(0)), summed after each batch has landed
-  float s1v[TM], s2v[TM];
+  // folded LayerNorm: the tile's rows' (mean, var) from the producers'
+  // slice partials.  Each wave takes BM / NW rows (no row loaded twice),
+  // the 4 lanes that share a row (lane >> 4) take slices q, q + 4, ...
+  // (D % 128 == 0, <= 32 slices), the loads issued behind the prologue's
+  // stage 0 whose wait covers them; Chan et al.'s merge, then (mean, var)
+  // to LDS behind the ring -- the prologue barrier publishes them.
   float4 c1v[TN];  // lnc1 of this lane's columns (an epilogue load would cost every tile an L2 round trip)
   auto ln_partial_loads = [&] {
-    if constexpr (AM == A_DENSE && (EM == E_QKV || EM == E_STORE)) {
+    if constexpr (LNF) {
+#ifdef MDE_FOLD_EXP  // timing experiment: no partial / c1 loads (wrong results)
       if (p.lnst_in) {
+#pragma unroll
+        for (int j = 0; j < TN; ++j) c1v[j] = float4{0.f, 0.f, 0.f, 0.f};
+        for (int r = tid; r < BM; r += NT)
+          *reinterpret_cast<float2*>(smem + SG * STAGE + r * 8) = make_float2(0.f, 1.f);
+      }
+      if (false) {
+#else
+      if (p.lnst_in) {
+#endif
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int n = n0 + wn * TN * 16 + j * 16 + (lane >> 4) * 4;
@@ -327,52 +340,40 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR gemm_kernel(co
         }
         const float2* st2 = reinterpret_cast<const float2*>(p.lnst_in);
         const float invd = 1.f / (float)(p.lnst_ns * 32);
-        // <= 16 slices (D <= 512): every row at once, 4 loads per row;
-        // up to 32 (D 1024): two rows at a time, 8 loads per row
-        auto rows = [&](auto kper_tag, int i0, int ni) {
-          constexpr int KP = decltype(kper_tag)::value;
-          float2 t[4][KP];
+        const int kp = p.lnst_ns >> 2;  // slices per lane (wave-uniform)
+        constexpr int RPW = BM / NW;    // rows per wave: 16 or 32
+        constexpr int G = (RPW + 15) / 16;
+        // all loads first, unpredicated (slices past kp re-read slice q, an
+        // L1 hit, and are masked below): one latency round trip, no branches
+        float2 t[G][8];
 #pragma unroll
-          for (int ii = 0; ii < 4; ++ii) {
-            if (ii >= ni) break;
-            const int m = m0 + wm * TM * 16 + (i0 + ii) * 16 + (lane & 15);
-            const int mc = m < p.M ? m : p.M - 1;
+        for (int g = 0; g < G; ++g) {
+          const int m = m0 + wave * RPW + g * 16 + (lane & 15);
+          const int mc = m < p.M ? m : p.M - 1;
 #pragma unroll
-            for (int k = 0; k < KP; ++k) {
-              const int sl = (lane >> 4) + 4 * k;
-              t[ii][k] = st2[(size_t)(sl < p.lnst_ns ? sl : 0) * p.lnst_rows + mc];
-            }
+          for (int k = 0; k < 8; ++k) {
+            const int sl = (lane >> 4) + (k < kp ? 4 * k : 0);
+            t[g][k] = st2[(size_t)sl * p.lnst_rows + mc];
           }
-          // Chan et al.'s merge of the slices' (sum, M2): the row mean
-          // first (4-lane xor-shuffle), then M2 = sum_s M2_s + 32 (mean_s -
-          // mean)^2 -- no E[x^2] - mean^2 cancellation
+        }
 #pragma unroll
-          for (int ii = 0; ii < 4; ++ii) {
-            if (ii >= ni) break;
-            float s1 = 0.f;
+        for (int g = 0; g < G; ++g) {
+          const int r = wave * RPW + g * 16 + (lane & 15);
+          float s1 = 0.f;
 #pragma unroll
-            for (int k = 0; k < KP; ++k) s1 += (lane >> 4) + 4 * k < p.lnst_ns ? t[ii][k].x : 0.f;
-            s1 += __shfl_xor(s1, 16);
-            s1 += __shfl_xor(s1, 32);
-            const float mean = s1 * invd;
-            float m2 = 0.f;
+          for (int k = 0; k < 8; ++k) s1 += k < kp ? t[g][k].x : 0.f;
+          s1 += __shfl_xor(s1, 16);
+          s1 += __shfl_xor(s1, 32);
+          const float mean = s1 * invd;
+          float m2 = 0.f;
 #pragma unroll
-            for (int k = 0; k < KP; ++k) {
-              const float d = t[ii][k].x * (1.f / 32.f) - mean;
-              m2 += (lane >> 4) + 4 * k < p.lnst_ns ? t[ii][k].y + 32.f * d * d : 0.f;
-            }
-            m2 += __shfl_xor(m2, 16);
-            m2 += __shfl_xor(m2, 32);
-            s1v[i0 + ii] = mean;
-            s2v[i0 + ii] = m2 * invd;  // variance
+          for (int k = 0; k < 8; ++k) {
+            const float d = t[g][k].x * (1.f / 32.f) - mean;
+            m2 += k < kp ? t[g][k].y + 32.f * d * d : 0.f;
           }
-        };
-        if (p.lnst_ns <= 16) {
-          rows(std::integral_constant<int, 4>{}, 0, TM < 4 ? TM : 4);
-          if constexpr (TM > 4) rows(std::integral_constant<int, 4>{}, 4, TM - 4);
-        } else {
-#pragma unroll
-          for (int i0 = 0; i0 < TM; i0 += 2) rows(std::integral_constant<int, 8>{}, i0, TM - i0 < 2 ? TM - i0 : 2);
+          m2 += __shfl_xor(m2, 16);
+          m2 += __shfl_xor(m2, 32);
+          if ((lane >> 4) == 0) *reinterpret_cast<float2*>(smem + SG * STAGE + r * 8) = make_float2(mean, m2 * invd);
         }
       }
     }
@@ -416,12 +417,12 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR gemm_kernel(co
   // slices' (sum, M2) by Chan et al.'s pairwise merge, fp32.
   if constexpr (AM == A_DENSE && (EM == E_QKV || EM == E_STORE)) {
     if (p.lnst_in) {
-      // s1v / s2v: the rows' mean and variance, merged in the prologue
-      // (ln_partial_loads)
+      // the rows' (mean, var), merged in the prologue (ln_partial_loads)
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
-        const float mean = s1v[i];
-        const float rstd = rsqrtf(s2v[i] + p.ln_eps);
+        const float2 mv = *reinterpret_cast<const float2*>(smem + SG * STAGE + (wm * TM * 16 + i * 16 + (lane & 15)) * 8);
+        const float mean = mv.x;
+        const float rstd = rsqrtf(mv.y + p.ln_eps);
         const float nm = -rstd * mean;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -581,7 +582,8 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
   if (p.lnst_out || p.lnst_in) {
     // folded LayerNorm: the 128^2 / 64^2 kernels of this file (partials per
     // 32-column slice from the LDS-staged epilogue, the fold after the main loop)
-    if ((p.lnst_ns * 32 != (p.lnst_out ? p.N : p.K)) || (p.lnst_in && (p.lnst_ns > 32 || p.lnst_rows != p.M)) ||
+    if ((p.lnst_ns * 32 != (p.lnst_out ? p.N : p.K)) ||
+        (p.lnst_in && (p.lnst_ns > 32 || (p.lnst_ns & 3) || p.lnst_rows != p.M)) ||
         (p.lnst_out && p.lnst_rows < (p.emode == E_PATCH ? p.M / p.npatch * p.T : p.M)) || (p.lnst_in && (!p.lnc1 || p.amode != A_DENSE)) ||
         (p.lnst_out && !p.xh))
       return hipErrorInvalidValue;

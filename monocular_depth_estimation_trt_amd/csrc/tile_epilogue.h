@@ -209,11 +209,23 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
     }
     auto phys = [&](int row, int ch) { return row * (C * 4) + ((ch ^ (row & (CHR >= 8 ? 7 : CHR - 1))) << 4); };
     // ---- phase 1: accumulators (+bias, activation) -> LDS ----
+    // bias for all TN column groups in one batch of unpredicated loads (a
+    // predicated load per group costs one serialised round trip each)
+    float4 bias[TN];
+    if (p.bias) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int n = n0w + j * 16 + (lane >> 4) * 4;
+        const int nc = n < p.N ? n : 0;
+        bias[j] = *reinterpret_cast<const float4*>(p.bias + (EM == E_CONVT ? nc % p.cout : nc));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < TN; ++j) bias[j] = float4{0.f, 0.f, 0.f, 0.f};
+    }
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
-      const int n = n0w + j * 16 + (lane >> 4) * 4;
-      float4 bn = {0.f, 0.f, 0.f, 0.f};
-      if (p.bias && n < p.N) bn = *reinterpret_cast<const float4*>(p.bias + (EM == E_CONVT ? n % p.cout : n));
+      const float4 bn = bias[j];  // columns n >= N are computed but never stored
 #pragma unroll
       for (int i = 0; i < TM; ++i) {
         f32x4 v = acc[i][j];

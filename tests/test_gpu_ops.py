@@ -349,7 +349,7 @@ def test_linear_residual_f16(gpu, m, n, k):
     close(part, ln_partials_ref(xh.cpu()).float(), 1e-5, 1e-3, "ln partials")
 
 
-@pytest.mark.parametrize("m,n,k,act", [(300, 1152, 384, 0), (38360, 1536, 384, 2), (1370, 2048, 512, 2), (1370, 3072, 1024, 2), (10960, 4096, 1024, 2),
+@pytest.mark.parametrize("m,n,k,act", [(300, 1152, 384, 0), (38360, 1536, 384, 2), (1370, 2048, 512, 2), (1370, 3072, 1024, 2), (10960, 4096, 1024, 2), (2740, 3072, 768, 0),
                                        (5, 64, 384, 0)])
 def test_linear_lnfold(gpu, m, n, k, act):
     """LayerNorm folded into the next linear: act(LN(x) W^T + b) from the
