@@ -186,6 +186,16 @@ int mde_op_patch_embed(const float* img, int batch, int h, int w, const void* w_
 int mde_op_conv3x3(const void* in_f16, int batch, int h, int w, int cin, const void* w_f16, int ldw, int cout,
                    int stride, int relu_in, const float* bias, int act, const void* res0_f16,
                    const void* res1_f16, void* out_f16, void* stream);
+/* mde_op_conv3x3 / mde_op_linear (E_STORE) with an fp32 split-K workspace of
+ * ws_floats elements: grids too small to fill the chip cut the K loop into
+ * slices (partials summed in slice order, then the epilogue); *slices (may be
+ * null) receives the slice count taken, 1 = no split.  The engine gives its
+ * DPT convs such a workspace (small batches). */
+int mde_op_conv3x3_ws(const void* in_f16, int batch, int h, int w, int cin, const void* w_f16, int ldw, int cout,
+                      int stride, int relu_in, const float* bias, int act, const void* res0_f16,
+                      const void* res1_f16, void* out_f16, float* ws, size_t ws_floats, int* slices, void* stream);
+int mde_op_linear_ws(const void* a_f16, int lda, const void* w_f16, int ldw, int m, int n, int k, const float* bias,
+                     int act, void* out_f16, int ldo, float* ws, size_t ws_floats, int* slices, void* stream);
 int mde_op_conv3x3_up(const void* in_f16, int batch, int sh, int sw, int cin, int uh, int uw, const void* w_f16,
                       int ldw, int cout, const float* bias, int act, void* out_f16, void* stream);
 int mde_op_conv_transpose(const void* in_f16, int batch, int h, int w, int cin, const void* w_f16, int ldw,

@@ -102,6 +102,10 @@ PROTOTYPES = {
                            c_void_p, c_void_p, c_void_p],
     "mde_op_conv3x3": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                        c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "mde_op_conv3x3_ws": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                          c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, P(c_int), c_void_p],
+    "mde_op_linear_ws": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int,
+                         c_void_p, c_size_t, P(c_int), c_void_p],
     "mde_op_conv3x3_up": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_void_p,
                           c_int, c_void_p, c_void_p],
     "mde_op_conv_transpose": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p,

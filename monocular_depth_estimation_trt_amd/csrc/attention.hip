@@ -54,6 +54,9 @@ constexpr int KT = 64;            // keys per tile (and Tpad granularity)
 constexpr int TILE_B = KT * 128;  // bytes of one K (or V^T) tile image: 64 rows x 128 B
 constexpr int SLOT = 2 * TILE_B;  // K + V^T
 constexpr int QW = 32;            // queries per wave (one 32-column MFMA block)
+#ifndef ATTN_RING
+#define ATTN_RING 2               // K/V^T ring depth (tiles; R-1 in flight while one is computed)
+#endif
 
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 
@@ -113,14 +116,16 @@ struct SplitWs {
   int tiles = 0;        // key tiles per split
 };
 
-template <int NW, bool SPLIT>
+template <int NW, bool SPLIT, int R>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4, 8)))
 attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16* __restrict__ vt,
                 f16* __restrict__ o, int H, int T, int Tpad, int ldo, SplitWs ws) {
   constexpr int BQ = QW * NW;    // queries per workgroup
   constexpr int INS = 8 / NW;    // glds instructions per wave per image (8 per 64-row image)
+  constexpr int PER_TILE = 2 * INS;  // vmcnt entries one tile adds per wave (K + V^T)
   static_assert(NW == 4 || NW == 8, "waves per workgroup");
-  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
+  static_assert(R >= 2 && R <= 4, "ring depth");
+  __shared__ __attribute__((aligned(16))) char smem[R * SLOT];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -183,8 +188,18 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
     acc[1][r] = 0.f;
   }
 
-  issue(kt0, 0);
-  wait_vm_n<0>();
+  // wait until tile `kt` has landed, given the tiles issued after it: at
+  // most `after` more tiles (0 .. R-2) may stay in flight
+  auto wait_tiles = [&](int after) {
+    if (R > 3 && after >= 2) wait_vm_n<(R > 3 ? 2 : 0) * PER_TILE>();
+    else if (R > 2 && after >= 1) wait_vm_n<(R > 2 ? 1 : 0) * PER_TILE>();
+    else wait_vm_n<0>();
+  };
+  // prologue: R-1 tiles in flight, then tile kt0 landed
+#pragma unroll
+  for (int i = 0; i < R - 1; ++i)
+    if (kt0 + i < kt1) issue(kt0 + i, i);
+  wait_tiles(min(kt1, kt0 + R - 1) - 1 - kt0);
   lds_barrier();
 
   auto tile = [&](int kt, auto slot_tag, auto first_tag) {
@@ -260,26 +275,34 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
     }
   };
 
-  // tile kt lives in ring slot (kt - kt0) & 1; the loop is unrolled over the
-  // two slots so every LDS address is lane base + immediate.  Tile kt+1 is
-  // issued into the other slot (released by the previous barrier) before
-  // tile kt is computed, and must land before the barrier that ends the step.
+  // tile kt lives in ring slot (kt - kt0) % R; the loop is unrolled over the
+  // R slots so every LDS address is lane base + immediate.  Step kt issues
+  // tile kt+R-1 into the slot of tile kt-1 (released by the previous
+  // barrier), computes tile kt, and waits -- counted, leaving the newer
+  // tiles in flight -- for tile kt+1 before the barrier that ends the step.
   auto step = [&](int kt, auto slot_tag, auto first_tag) {
     constexpr int SL = decltype(slot_tag)::value;
-    if (kt + 1 < kt1) issue(kt + 1, SL ^ 1);
+    if (kt + R - 1 < kt1) issue(kt + R - 1, (SL + R - 1) % R);
     if (active) tile(kt, slot_tag, first_tag);
-    wait_vm_n<0>();
+    wait_tiles(min(kt1 - 1, kt + R - 1) - (kt + 1));
     lds_barrier();
   };
   using S0 = std::integral_constant<int, 0>;
-  using S1 = std::integral_constant<int, 1>;
+  using S1 = std::integral_constant<int, 1 % R>;
+  using S2 = std::integral_constant<int, 2 % R>;
+  using S3 = std::integral_constant<int, 3 % R>;
+  using NF = std::false_type;
   step(kt0, S0{}, std::true_type{});
   int kt = kt0 + 1;
-  for (; kt + 2 <= kt1; kt += 2) {
-    step(kt, S1{}, std::false_type{});
-    step(kt + 1, S0{}, std::false_type{});
+  for (; kt + R <= kt1; kt += R) {
+    step(kt, S1{}, NF{});
+    step(kt + 1, S2{}, NF{});
+    if constexpr (R > 2) step(kt + 2, S3{}, NF{});
+    if constexpr (R > 3) step(kt + 3, S0{}, NF{});
   }
-  if (kt < kt1) step(kt, S1{}, std::false_type{});
+  if (kt < kt1) step(kt, S1{}, NF{});
+  if (R > 2 && kt + 1 < kt1) step(kt + 1, S2{}, NF{});
+  if (R > 3 && kt + 2 < kt1) step(kt + 2, S3{}, NF{});
   if (!active) return;
 
   if constexpr (SPLIT) {
@@ -361,7 +384,7 @@ __global__ void __launch_bounds__(256) attn_combine_kernel(SplitWs ws, int S, in
   *reinterpret_cast<f16x8*>(o + ((size_t)b * T + qi) * ldo + h * 64 + 8 * d8) = v;
 }
 
-template <int NW>
+template <int NW, int R>
 hipError_t run_attn(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T, int Tpad, int ldo,
                     float* ws, size_t ws_bytes, int split, hipStream_t st) {
   constexpr int BQ = QW * NW;
@@ -379,7 +402,7 @@ hipError_t run_attn(const h16* q, const h16* k, const h16* vt, h16* o, int B, in
     if (S > 1 && rows * 66 * sizeof(float) <= ws_bytes) {
       w.o = ws;
       w.ml = ws + rows * 64;
-      hipLaunchKernelGGL((attn_fwd_kernel<NW, true>), dim3(nqb, B * H, S), dim3(NW * 64), 0, st, cq, ck, cv, co, H, T,
+      hipLaunchKernelGGL((attn_fwd_kernel<NW, true, R>), dim3(nqb, B * H, S), dim3(NW * 64), 0, st, cq, ck, cv, co, H, T,
                          Tpad, ldo, w);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
@@ -389,7 +412,7 @@ hipError_t run_attn(const h16* q, const h16* k, const h16* vt, h16* o, int B, in
       return hipGetLastError();
     }
   }
-  hipLaunchKernelGGL((attn_fwd_kernel<NW, false>), dim3(nqb, B * H), dim3(NW * 64), 0, st, cq, ck, cv, co, H, T, Tpad,
+  hipLaunchKernelGGL((attn_fwd_kernel<NW, false, R>), dim3(nqb, B * H), dim3(NW * 64), 0, st, cq, ck, cv, co, H, T, Tpad,
                      ldo, SplitWs{});
   return hipGetLastError();
 }
@@ -408,13 +431,15 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
   // the 16-B output stores need ldo % 8 == 0 (and a 16-B aligned o)
   if (Tpad % KT || Tpad < ((T + KT - 1) / KT) * KT || (ldo & 7) || ((uintptr_t)o & 15)) return hipErrorInvalidValue;
   const int nkt = (T + KT - 1) / KT;
-  // MDE_ATTN_CFG = <waves>[s<split>] ("8", "4", "4s8", ...): tuning override
+  // MDE_ATTN_CFG = <waves>[s<split>][r<ring>] ("8", "4", "4s8", "8r3", ...): tuning override
   static const char* forced = getenv("MDE_ATTN_CFG");
-  int nw = 0, split = 1;
+  int nw = 0, split = 1, ring = ATTN_RING;
   if (forced) {
     nw = atoi(forced);
     const char* sp = strchr(forced, 's');
     split = sp ? atoi(sp + 1) : 1;
+    const char* rp = strchr(forced, 'r');
+    if (rp) ring = atoi(rp + 1);
   }
   if (nw != 4 && nw != 8) {
     // 256-query workgroups share each K/V^T tile over 8 waves once the grid
@@ -428,8 +453,14 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
     if (nw == 4 && g128 < 256)
       while (split < 8 && g128 * split * 2 <= 640 && nkt >= 3 * split * 2) split *= 2;
   }
-  if (nw == 8) return run_attn<8>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, split, st);
-  return run_attn<4>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, split, st);
+  if (nw == 8) {
+    if (ring == 4) return run_attn<8, 4>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, split, st);
+    if (ring == 3) return run_attn<8, 3>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, split, st);
+    return run_attn<8, 2>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, split, st);
+  }
+  if (ring == 4) return run_attn<4, 4>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, split, st);
+  if (ring == 3) return run_attn<4, 3>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, split, st);
+  return run_attn<4, 2>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, split, st);
 }
 
 }  // namespace mde

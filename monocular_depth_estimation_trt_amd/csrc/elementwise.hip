@@ -445,6 +445,65 @@ hipError_t launch_splitk_resid(const float* P, int S, int M, int N, const float*
   return hipGetLastError();
 }
 
+namespace {
+// second half of the E_STORE split-K path (gemm.hip launch_split_store): one
+// thread per 8 columns of a row, slices added in order 0..S-1, then the
+// E_STORE epilogue of tile_epilogue.h (bias, activation, then the residual
+// adds, one rounding to f16)
+__global__ void splitk_store_kernel(const float* __restrict__ P, int S, int M, int N, GemmParams p) {
+  const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const int n8 = N >> 3;
+  if (i >= (long long)M * n8) return;
+  const int m = (int)(i / n8), n = (int)(i - (long long)m * n8) * 8;
+  const size_t plane = (size_t)M * N;
+  const float* src = P + (size_t)m * N + n;
+  float4 a0 = *reinterpret_cast<const float4*>(src), a1 = *reinterpret_cast<const float4*>(src + 4);
+  for (int s = 1; s < S; ++s) {
+    const float4 b0 = *reinterpret_cast<const float4*>(src + s * plane);
+    const float4 b1 = *reinterpret_cast<const float4*>(src + s * plane + 4);
+    a0.x += b0.x; a0.y += b0.y; a0.z += b0.z; a0.w += b0.w;
+    a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
+  }
+  float v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
+  if (p.bias) {
+    const float4 c0 = *reinterpret_cast<const float4*>(p.bias + n), c1 = *reinterpret_cast<const float4*>(p.bias + n + 4);
+    v[0] += c0.x; v[1] += c0.y; v[2] += c0.z; v[3] += c0.w;
+    v[4] += c1.x; v[5] += c1.y; v[6] += c1.z; v[7] += c1.w;
+  }
+  if (p.act == ACT_RELU) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+  } else if (p.act == ACT_GELU) {
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] = gelu_erf(v[r]);
+  }
+  const size_t o = (size_t)m * p.ldo + n;
+  if (p.res0) {
+    const size_t ro = p.res0_rows > 0 ? (size_t)(m % p.res0_rows) * p.ldo + n : o;
+    const f16x8 r0 = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res0) + ro);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] += p.res0_relu ? fmaxf((float)r0[r], 0.f) : (float)r0[r];
+  }
+  if (p.res1) {
+    const f16x8 r1 = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res1) + o);
+#pragma unroll
+    for (int r = 0; r < 8; ++r) v[r] += (float)r1[r];
+  }
+  f16x8 h;
+#pragma unroll
+  for (int r = 0; r < 8; ++r) h[r] = (f16)v[r];
+  *reinterpret_cast<f16x8*>(reinterpret_cast<f16*>(p.out16) + o) = h;
+}
+}  // namespace
+
+hipError_t launch_splitk_store(const float* P, int S, const GemmParams& p, hipStream_t st) {
+  if (S < 1 || (p.N & 7) || (p.ldo & 7) || !p.out16 || p.ldo < p.N) return hipErrorInvalidValue;
+  const long long n = (long long)p.M * (p.N >> 3);
+  if (n <= 0) return hipSuccess;
+  hipLaunchKernelGGL(splitk_store_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, P, S, p.M, p.N, p);
+  return hipGetLastError();
+}
+
 hipError_t launch_resize(const h16* in, h16* out, int B, int ih, int iw, int C, int oh, int ow, hipStream_t st) {
   if (C & 7) return hipErrorInvalidValue;
   const long long n = (long long)B * oh * ow * (C >> 3);

@@ -217,6 +217,7 @@ size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
   const int bsplit = std::min<int>(B, (256 + ((e.T + 127) / 128) * e.H - 1) / (((e.T + 127) / 128) * e.H));
   t.aws_bytes = bsplit >= 1 ? attention_split_ws_bytes(bsplit, e.H, e.T) : 0;
   t.aws = t.aws_bytes ? a.f(t.aws_bytes / sizeof(float)) : nullptr;
+  t.sws = a.f(kSplitWsFloats);
   if (b) *b = t;
   return a.off;
 }
@@ -265,6 +266,7 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
   DAV2Buf& b = c.b;
 
   const bool fold = b.st != nullptr;
+  split_ws = b.sws;
   const float* cls_st = fold ? w32("pos.cls.st") : nullptr;
   step("patch_prep", [&] {
     if (cf.input_u8)
@@ -1282,6 +1284,61 @@ int mde_op_conv3x3(const void* in, int batch, int h, int w, int cin, const void*
   g.out16 = (h16*)out;
   g.ldo = cout;
   OP_RET(launch_gemm(g, (hipStream_t)st), "conv3x3");
+}
+
+int mde_op_conv3x3_ws(const void* in, int batch, int h, int w, int cin, const void* wt, int ldw, int cout, int stride,
+                      int relu_in, const float* bias, int act, const void* res0, const void* res1, void* out,
+                      float* ws, size_t ws_floats, int* slices, void* st) {
+  if (!in || !wt || !out || (!ws && ws_floats)) return fail(MDE_ERR_ARG, "null argument");
+  if (stride != 1 && stride != 2) return fail(MDE_ERR_ARG, "stride must be 1 or 2");
+  GemmParams g;
+  g.amode = A_CONV3;
+  g.A = (const h16*)in;
+  g.cb = batch;
+  g.ch = h;
+  g.cw = w;
+  g.cc = cin;
+  g.stride = stride;
+  g.oh = (h - 1) / stride + 1;
+  g.ow = (w - 1) / stride + 1;
+  g.W = (const h16*)wt;
+  g.ldw = ldw;
+  g.M = batch * g.oh * g.ow;
+  g.N = cout;
+  g.K = 9 * cin;
+  g.relu_in = relu_in;
+  g.bias = bias;
+  g.act = act;
+  g.res0 = (const h16*)res0;
+  g.res1 = (const h16*)res1;
+  g.out16 = (h16*)out;
+  g.ldo = cout;
+  g.partial = ws;
+  g.partial_cap = ws_floats;
+  if (slices) *slices = gemm_store_split_slices(g);
+  OP_RET(launch_gemm(g, (hipStream_t)st), "conv3x3_ws");
+}
+
+int mde_op_linear_ws(const void* a, int lda, const void* wt, int ldw, int m, int n, int k, const float* bias, int act,
+                     void* out, int ldo, float* ws, size_t ws_floats, int* slices, void* st) {
+  if (!a || !wt || !out || (!ws && ws_floats)) return fail(MDE_ERR_ARG, "null argument");
+  GemmParams g;
+  g.amode = A_DENSE;
+  g.A = (const h16*)a;
+  g.lda = lda;
+  g.W = (const h16*)wt;
+  g.ldw = ldw;
+  g.M = m;
+  g.N = n;
+  g.K = k;
+  g.bias = bias;
+  g.act = act;
+  g.out16 = (h16*)out;
+  g.ldo = ldo;
+  g.partial = ws;
+  g.partial_cap = ws_floats;
+  if (slices) *slices = gemm_store_split_slices(g);
+  OP_RET(launch_gemm(g, (hipStream_t)st), "linear_ws");
 }
 
 int mde_op_conv3x3_up(const void* in, int batch, int sh, int sw, int cin, int uh, int uw, const void* wt, int ldw,

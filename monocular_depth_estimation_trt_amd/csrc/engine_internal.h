@@ -38,7 +38,12 @@ struct DAV2Buf {
   float* aws;       // attention split-KV partials (batches whose grid splits, else null)
   size_t aws_bytes;
   float* st;        // folded-LN partials [B*T][D/32][2] (f16 residual + folded pack, else null)
+  float* sws;       // E_STORE split-K partials (GemmParams::partial_cap = kSplitWsFloats)
 };
+
+// fp32 elements of a context's E_STORE split-K workspace (launch_gemm bounds
+// slices x M x N by it; the largest split the policy picks is ~4.2 M)
+constexpr size_t kSplitWsFloats = size_t(5) << 20;
 
 // Depth Pro activations (depth_pro.hip plan_arena_dp).  Token buffers are
 // sized for the patch encoder (35 sequences per image), the largest of the
@@ -257,7 +262,17 @@ struct Runner {
     return g;
   }
 
+  // E_STORE split-K workspace for launch_gemm's small-grid policy (null: never split)
+  float* split_ws = nullptr;
+
   void gemm(const char* name, const GemmParams& g) {
+    if (split_ws && g.emode == E_STORE && !g.partial) {
+      GemmParams q = g;
+      q.partial = split_ws;
+      q.partial_cap = kSplitWsFloats;
+      step(name, [&] { return launch_gemm(q, st); });
+      return;
+    }
     step(name, [&] { return launch_gemm(g, st); });
   }
 

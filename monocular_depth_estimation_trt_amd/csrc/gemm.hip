@@ -189,10 +189,20 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR gemm_kernel(co
       urow[i] = reinterpret_cast<const f16*>(p.A) + (size_t)b * p.ch * p.cw * p.cc;
     }
   }
-  // conv K position (tap, c0) of this lane's chunk, advanced by BK per step
-  int tap = 0, c0 = (AM == A_CONV3_UP ? ulch : lch) * 8;
+  // K-tiles [kt0, kt0 + nk): all of K, or this workgroup's split-K slice
+  int nk = (p.K + BK - 1) / BK, kt0 = 0;
+  if constexpr (EM == E_PARTIAL) {
+    const int per = (nk + (int)gridDim.y - 1) / (int)gridDim.y;
+    kt0 = (int)blockIdx.y * per;
+    nk = min(nk - kt0, per);  // >= 1: the launcher uses at most nk slices of ceil(nk / S) tiles
+  }
+
+  // conv K position (tap, c0) of this lane's chunk at K-tile kt0, advanced by
+  // BK per step
+  int tap = 0, c0 = kt0 * BK + (AM == A_CONV3_UP ? ulch : lch) * 8;
   if constexpr (AM != A_DENSE) {
-    while (c0 >= p.cc) { c0 -= p.cc; ++tap; }
+    tap = c0 / p.cc;
+    c0 -= tap * p.cc;
   }
   float usy = 0.f, usx = 0.f;
   if constexpr (AM == A_CONV3_UP) {
@@ -205,14 +215,6 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR gemm_kernel(co
   auto aslot = [&](int i) { return (wave + i * NW) * G::RW * ROWB; };  // LDS row offset of slot i
 
   f16x8 ru[UPC];
-
-  // K-tiles [kt0, kt0 + nk): all of K, or this workgroup's split-K slice
-  int nk = (p.K + BK - 1) / BK, kt0 = 0;
-  if constexpr (EM == E_PARTIAL) {
-    const int per = (nk + (int)gridDim.y - 1) / (int)gridDim.y;
-    kt0 = (int)blockIdx.y * per;
-    nk = min(nk - kt0, per);  // >= 1: the launcher uses at most nk slices of ceil(nk / S) tiles
-  }
 
   auto issue = [&](int kt, int buf) {
     char* sbase = smem + buf * STAGE;
@@ -540,7 +542,56 @@ bool prefer_im2col(const GemmParams& p) {
   return p.cc >= 256 && (double)p.oh * p.ow < 0.6 * tiles;
 }
 
+// E_STORE split-K: slices of the K loop on 64^2 tiles into the fp32
+// workspace, then launch_splitk_store sums them in slice order and runs the
+// epilogue (deterministic).  For grids that leave most of the chip idle: the
+// small-batch DPT convs on 19^2 / 37^2 / 74^2 maps walk K = 9 Cin (up to
+// 9216) in a few dozen workgroups (ViT-L B = 1: layer3_rn 30 direct-conv
+// workgroups x 16 channel chunks, 129 us).  Returns the slice count (1 = no split).
+int store_split_slices(const GemmParams& p) {
+  if (p.emode != E_STORE || !p.partial || p.partial_cap == 0 || p.lnst_in || p.lnst_out) return 1;
+  if (p.amode != A_DENSE && p.amode != A_CONV3) return 1;
+  if (p.amode == A_CONV3 && p.stride != 1 && p.stride != 2) return 1;
+  const char* off = getenv("MDE_SPLITK");  // read per call: tests toggle it (captured graphs keep their choice)
+  if (off && off[0] == '0') return 1;
+  const int nk = (p.K + 63) / 64;
+  const long long t64 = (long long)((p.M + 63) / 64) * ((p.N + 63) / 64);
+  // workgroups of the unsplit launch
+  long long wgs;
+  if (p.amode == A_CONV3 && conv_direct_supported(p) && !prefer_im2col(p)) {
+    const int bn = p.N <= 32 ? 32 : (p.N <= 64 ? 64 : 128);
+    wgs = (long long)p.cb * ((p.oh + 7) / 8) * ((p.ow + 15) / 16) * ((p.N + bn - 1) / bn);
+  } else {
+    const long long big = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128);
+    wgs = big >= 240 ? big : t64;
+  }
+  if (wgs >= 256 || nk < 8) return 1;
+  int S = (int)((512 + t64 - 1) / t64);
+  S = S < nk / 4 ? S : nk / 4;  // >= 4 K-steps per slice
+  S = S < 16 ? S : 16;
+  while (S > 1 && (size_t)S * p.M * p.N > p.partial_cap) --S;
+  if (S <= 1) return 1;
+  const int per = (nk + S - 1) / S;
+  return (nk + per - 1) / per;  // every slice non-empty
+}
+
+template <int AM>
+hipError_t launch_split_store(const GemmParams& p, int S, hipStream_t st) {
+  GemmParams q = p;
+  q.emode = E_PARTIAL;
+  q.x32 = p.partial;
+  q.ldo = p.N;
+  const unsigned tiles = (unsigned)(((p.M + 63) / 64) * ((p.N + 63) / 64));
+  hipLaunchKernelGGL((gemm_kernel<64, 64, MDE_GEMM_BK, 2, 2, AM, E_PARTIAL>), dim3(tiles, (unsigned)S), dim3(256), 0,
+                     st, q);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return launch_splitk_store(p.partial, S, p, st);
+}
+
 }  // namespace
+
+int gemm_store_split_slices(const GemmParams& p) { return store_split_slices(p); }
 
 hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
   if (p.M <= 0 || p.N <= 0) return hipSuccess;
@@ -555,6 +606,10 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
   if (p.emode == E_CONVT && ((p.cout & 7) || (p.ldo & 7) || p.ldo < p.cout || ((uintptr_t)p.out16 & 15)))
     return hipErrorInvalidValue;
   if (p.emode == E_HEAD && (p.N != 32 || p.amode == A_DENSE)) return hipErrorInvalidValue;
+  if (const int S = store_split_slices(p); S > 1) {
+    if ((p.ldo & 7) || ((uintptr_t)p.partial & 15)) return hipErrorInvalidValue;
+    return p.amode == A_DENSE ? launch_split_store<A_DENSE>(p, S, st) : launch_split_store<A_CONV3>(p, S, st);
+  }
   if (p.amode != A_DENSE && conv_direct_supported(p) && !getenv_im2col() && !prefer_im2col(p))
     return launch_conv3(p, st);
   if ((p.emode == E_RESID || p.emode == E_PATCH) && p.xh && ((uintptr_t)p.xh & 15)) return hipErrorInvalidValue;

@@ -66,6 +66,11 @@ struct GemmParams {
   // workspace [splitk][M][N]; the K range is cut into splitk slices whose
   // partial sums are added in slice order by a second kernel (deterministic)
   int splitk = 1; float* partial = nullptr;
+  // E_STORE split-K (dense and 3x3-conv problems whose tile grid leaves most
+  // of the chip idle: small batches, the DPT's 19^2 / 37^2 maps): when
+  // partial_cap > 0 the launcher picks the slice count itself, bounded by
+  // partial_cap fp32 elements of `partial`
+  size_t partial_cap = 0;
   // LayerNorm folded across a GEMM boundary (DA-V2 f16-residual engines):
   //  * producer (E_RESID / E_PATCH over xh, and the split-K reduce): lnst_out
   //    = fp32 [lnst_ns][lnst_rows][2] -- per 32-column slice and token row
@@ -85,7 +90,13 @@ struct GemmParams {
 hipError_t launch_splitk_resid(const float* P, int S, int M, int N, const float* bias, const float* ls, float* x32,
                                h16* xh, int ldo, hipStream_t st, float* lnst_out = nullptr);  // lnst_out rows = M
 
+// out16 = E_STORE epilogue of (sum_{s<S} P[s][m][n]) (elementwise.hip): the
+// second half of the E_STORE split-K path
+hipError_t launch_splitk_store(const float* P, int S, const GemmParams& p, hipStream_t st);
+
 hipError_t launch_gemm(const GemmParams& p, hipStream_t st);
+// slices launch_gemm's E_STORE split-K policy picks for p (1 = no split)
+int gemm_store_split_slices(const GemmParams& p);
 
 // Direct 3x3 conv with an LDS halo patch (conv.hip); launch_gemm routes
 // A_CONV3 / A_CONV3_UP problems here when conv_direct_supported().

@@ -10,6 +10,8 @@ magnitude (stated per test).
 
 import math
 
+import ctypes as C
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -240,6 +242,57 @@ def test_conv3x3(gpu, B, h, w, cin, cout, stride, relu_in, act, nres):
     op("mde_op_conv3x3", ptr(nhwc(x).half().to(gpu)), B, h, w, cin, ptr(wp), wp.shape[1], cout, stride, relu_in,
        ptr(b.to(gpu)), act, ptr(rg[0]), ptr(rg[1]), ptr(out), stream())
     close(nchw(out), ref, 1e-2, 1e-2, f"conv3x3 {h}x{w} {cin}->{cout} s{stride}")
+
+
+# E_STORE split-K (launch_gemm's small-grid policy): the batch-1 ViT-L DPT
+# shapes -- layer4_rn (19^2, 1024 -> 256, im2col), layer3_rn (37^2, direct conv
+# grid), conv_s2 (37^2 -> 19^2, stride 2), an RCU conv with pre-ReLU, bias,
+# ReLU and two residual adds, layer2_rn (74^2, 512 -> 256)
+@pytest.mark.parametrize("B,h,w,cin,cout,stride,relu_in,act,nres",
+                         [(1, 19, 19, 1024, 256, 1, 0, 0, 0), (1, 37, 37, 1024, 256, 1, 0, 0, 0),
+                          (1, 37, 37, 1024, 1024, 2, 0, 0, 0), (1, 37, 37, 256, 256, 1, 1, 1, 2),
+                          (1, 74, 74, 512, 256, 1, 0, 0, 0), (2, 19, 19, 384, 64, 1, 1, 0, 1)])
+def test_conv3x3_splitk(gpu, B, h, w, cin, cout, stride, relu_in, act, nres):
+    x = rn(B, cin, h, w)
+    wt, b = rn(cout, cin, 3, 3, scale=(9 * cin) ** -0.5), rn(cout, scale=0.02)
+    xin = x.half().float()
+    ref = F.conv2d(F.relu(xin) if relu_in else xin, wt.half().float(), b, stride=stride, padding=1)
+    if act == 1:
+        ref = F.relu(ref)
+    res = [rn(*ref.shape) for _ in range(nres)]
+    for r in res:
+        ref = ref + r.half().float()
+    wp = conv_w(wt).to(gpu)
+    ho, wo = ref.shape[2], ref.shape[3]
+    rg = [nhwc(r).half().to(gpu) for r in res] + [None, None]
+    xg, bg = nhwc(x).half().to(gpu), b.to(gpu)
+    ws = torch.empty(5 << 20, dtype=torch.float32, device=gpu)
+    got = []
+    for cap in (0, ws.numel()):
+        out = torch.empty(B, ho, wo, cout, dtype=torch.float16, device=gpu)
+        sl = C.c_int(0)
+        op("mde_op_conv3x3_ws", ptr(xg), B, h, w, cin, ptr(wp), wp.shape[1], cout, stride, relu_in, ptr(bg), act,
+           ptr(rg[0]), ptr(rg[1]), ptr(out), ptr(ws if cap else None), cap, C.byref(sl), stream())
+        assert (sl.value > 1) == (cap > 0), f"split slices {sl.value} with workspace {cap}"
+        close(nchw(out), ref, 1e-2, 1e-2, f"conv3x3 split {sl.value} {h}x{w} {cin}->{cout} s{stride}")
+        got.append(out.float())
+    # the split only reassociates the fp32 sum
+    assert (got[0] - got[1]).abs().max().item() < 2e-2
+
+
+@pytest.mark.parametrize("m,n,k,act", [(1369, 256, 1024, 0), (361, 1024, 1024, 2), (1370, 384, 384, 1)])
+def test_linear_splitk(gpu, m, n, k, act):
+    a, w, b = rn(m, k), rn(n, k, scale=k ** -0.5), rn(n, scale=0.1)
+    ref = a.half().float() @ w.half().float().T + b
+    ref = F.relu(ref) if act == 1 else (F.gelu(ref) if act == 2 else ref)
+    wp = pad_w(w).to(gpu)
+    ws = torch.empty(5 << 20, dtype=torch.float32, device=gpu)
+    out = torch.empty(m, n, dtype=torch.float16, device=gpu)
+    sl = C.c_int(0)
+    op("mde_op_linear_ws", ptr(f16(a, gpu)), k, ptr(wp), wp.shape[1], m, n, k, ptr(b.to(gpu)), act, ptr(out), n,
+       ptr(ws), ws.numel(), C.byref(sl), stream())
+    assert sl.value > 1 or k < 512, f"expected a split, got {sl.value}"
+    close(out, ref, 1e-2, 1e-2, f"linear split {sl.value} {m}x{n}x{k} act{act}")
 
 
 @pytest.mark.parametrize("B,sh,sw,uh,uw,cin,cout", [(1, 10, 10, 19, 19, 64, 32), (2, 16, 12, 28, 21, 32, 64),
