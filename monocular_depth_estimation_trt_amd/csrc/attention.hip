@@ -36,9 +36,13 @@
 // running max and sum, and attn_combine_kernel merges them.
 //
 // Measured alternatives (MI355X, B = 28): two 32-query
-// sub-blocks per wave (256 VGPRs), 128-key tiles, a 3-slot ring, one-block
-// software pipelining and an 8-wave ping-pong of MFMA / softmax segments were
-// all slower than this form (110 us; the 16x16x32 predecessor ~120 us).
+// sub-blocks per wave (256 VGPRs), 128-key tiles, one-block software
+// pipelining, an 8-wave ping-pong of MFMA / softmax segments and a lagged
+// second half (waves 4-7 half a tile behind, carrying the scores across the
+// barrier: 155 vs 113 us -- 226 VGPRs, one workgroup per CU) were all slower
+// than this form; 3- and 4-deep K/V rings (MDE_ATTN_CFG=8r3 / 8r4) measure
+// the same as 2 (SQ counters: the waits are issue/dependency stalls, not
+// load latency).
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
@@ -125,6 +129,7 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
   constexpr int PER_TILE = 2 * INS;  // vmcnt entries one tile adds per wave (K + V^T)
   static_assert(NW == 4 || NW == 8, "waves per workgroup");
   static_assert(R >= 2 && R <= 4, "ring depth");
+  constexpr int DIST = R - 1;  // tiles in flight ahead of the one computed
   __shared__ __attribute__((aligned(16))) char smem[R * SLOT];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -189,109 +194,117 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
   }
 
   // wait until tile `kt` has landed, given the tiles issued after it: at
-  // most `after` more tiles (0 .. R-2) may stay in flight
+  // most `after` more tiles (0 .. DIST-1) may stay in flight
   auto wait_tiles = [&](int after) {
-    if (R > 3 && after >= 2) wait_vm_n<(R > 3 ? 2 : 0) * PER_TILE>();
-    else if (R > 2 && after >= 1) wait_vm_n<(R > 2 ? 1 : 0) * PER_TILE>();
+    if (DIST > 2 && after >= 2) wait_vm_n<(DIST > 2 ? 2 : 0) * PER_TILE>();
+    else if (DIST > 1 && after >= 1) wait_vm_n<(DIST > 1 ? 1 : 0) * PER_TILE>();
     else wait_vm_n<0>();
   };
-  // prologue: R-1 tiles in flight, then tile kt0 landed
+  // prologue: DIST tiles in flight, then tile kt0 landed
 #pragma unroll
-  for (int i = 0; i < R - 1; ++i)
+  for (int i = 0; i < DIST; ++i)
     if (kt0 + i < kt1) issue(kt0 + i, i);
-  wait_tiles(min(kt1, kt0 + R - 1) - 1 - kt0);
+  wait_tiles(min(kt1, kt0 + DIST) - 1 - kt0);
   lds_barrier();
 
-  auto tile = [&](int kt, auto slot_tag, auto first_tag) {
-    constexpr bool FIRST_TILE = decltype(first_tag)::value;
-    constexpr int slot = decltype(slot_tag)::value;  // compile-time: LDS offsets fold into ds_read immediates
-    const char* K_ = smem + slot * SLOT;
-    const char* V_ = K_ + TILE_B;
+  // S'^T[key][query] = K Q^T - m_run over the 32 keys of block kb2 of tile
+  // kt (4 dim k-steps); keys >= T -> -inf
+  auto scores = [&](const char* K_, int kt, int kb2, auto first_tag) {
+    constexpr bool FIRST = decltype(first_tag)::value;
+    f32x16 sc;
+    if constexpr (FIRST) {
 #pragma unroll
-    for (int kb2 = 0; kb2 < 2; ++kb2) {
-      const bool FIRST = FIRST_TILE && kb2 == 0;  // compile-time after unrolling
-      // S'^T[key][query] = K Q^T - m_run over 32 keys: 4 dim k-steps
-      f32x16 sc;
-      if (FIRST) {
+      for (int r = 0; r < 16; ++r) sc[r] = 0.f;
+    } else {
+      sc = negm;
+    }
+    const int krow = kb2 * 32 + l31;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) sc[r] = 0.f;
-      } else {
-        sc = negm;
-      }
-      const int krow = kb2 * 32 + l31;
+    for (int st = 0; st < 4; ++st) {
+      const f16x8 kf = *reinterpret_cast<const f16x8*>(K_ + swz(krow, 2 * st + hh));
+      sc = mfma32(kf, qf[st], sc);
+    }
+    if (kt * KT + kb2 * 32 + 32 > T) {  // last, partial block
+      const int key0 = kt * KT + kb2 * 32 + 4 * hh;
 #pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const f16x8 kf = *reinterpret_cast<const f16x8*>(K_ + swz(krow, 2 * st + hh));
-        sc = mfma32(kf, qf[st], sc);
-      }
-      if (kt * KT + kb2 * 32 + 32 > T) {  // last, partial block: keys >= T -> -inf
-        const int key0 = kt * KT + kb2 * 32 + 4 * hh;
+      for (int r = 0; r < 16; ++r)
+        if (key0 + (r & 3) + 8 * (r >> 2) >= T) sc[r] = -INFINITY;
+    }
+    return sc;
+  };
+  // online-softmax update and P.V of one block whose scores are sc (V_ = the
+  // V^T image of the block's tile)
+  auto softmax_pv = [&](f32x16 sc, const char* V_, int kb2, auto first_tag) {
+    constexpr bool FIRST = decltype(first_tag)::value;
+    // the lane's max over its 16 scores (v_max3 chain); the row max (partner
+    // lane l ^ 32) only when some row rescales
+    float mx = fmaxf(sc[0], sc[1]);
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-          if (key0 + (r & 3) + 8 * (r >> 2) >= T) sc[r] = -INFINITY;
-      }
-      // max over the lane's 16 scores (v_max3 chain) and its partner lane
-      float mx = fmaxf(sc[0], sc[1]);
-#pragma unroll
-      for (int r = 2; r < 16; r += 2) mx = fmaxf(fmaxf(mx, sc[r]), sc[r + 1]);
+    for (int r = 2; r < 16; r += 2) mx = fmaxf(fmaxf(mx, sc[r]), sc[r + 1]);
+    if (FIRST || __any(mx > RESCALE_T)) {
       mx = swap_max(mx);  // max of S' over the block (relative to m_run)
-      if (FIRST || __any(mx > RESCALE_T)) {
-        // the running max grows by delta >= 0: shift S', rescale O and l
-        const float delta = FIRST ? mx : fmaxf(mx, 0.f);
-        m_run += delta;
+      // the running max grows by delta >= 0: shift S', rescale O and l
+      const float delta = FIRST ? mx : fmaxf(mx, 0.f);
+      m_run += delta;
 #pragma unroll
-        for (int r = 0; r < 16; ++r) negm[r] = -m_run;
-        sc -= delta;
-        if (!FIRST) {
-          const float alpha = __builtin_amdgcn_exp2f(-delta);
-          l_run *= alpha;
-          acc[0] *= alpha;
-          acc[1] *= alpha;
-        }
-      }
-      // P = exp2(S'), row sums, and P^T as the PV B operand: registers
-      // 8s..8s+7 are k-step s (keys 16s + 8(j>>2) + 4hh + (j&3))
-      f16x8 pb[2];
-      float ls0, ls1;
-#pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const float p0 = __builtin_amdgcn_exp2f(sc[r]), p1 = __builtin_amdgcn_exp2f(sc[r + 1]);
-        ls0 = r ? ls0 + p0 : p0;
-        ls1 = r ? ls1 + p1 : p1;
-        pb[r >> 3][r & 7] = (f16)p0;
-        pb[r >> 3][(r & 7) + 1] = (f16)p1;
-      }
-      l_run += ls0 + ls1;
-      // O^T[dh][q] += V^T[dh][key] P^T[key][q]: two 32-row dh blocks x 2 key k-steps
-#pragma unroll
-      for (int db = 0; db < 2; ++db) {
-        const int vrow = db * 32 + l31;
-#pragma unroll
-        for (int g = 0; g < 2; ++g) {
-          const f16x8 vf = *reinterpret_cast<const f16x8*>(V_ + swz(vrow, 2 * (2 * kb2 + g) + hh));
-          acc[db] = mfma32(vf, pb[g], acc[db]);
-        }
+      for (int r = 0; r < 16; ++r) negm[r] = -m_run;
+      sc -= delta;
+      if (!FIRST) {
+        const float alpha = __builtin_amdgcn_exp2f(-delta);
+        l_run *= alpha;
+        acc[0] *= alpha;
+        acc[1] *= alpha;
       }
     }
+    // P = exp2(S'), row sums, and P^T as the PV B operand: registers
+    // 8s..8s+7 are k-step s (keys 16s + 8(j>>2) + 4hh + (j&3))
+    f16x8 pb[2];
+    float ls0, ls1;
+#pragma unroll
+    for (int r = 0; r < 16; r += 2) {
+      const float p0 = __builtin_amdgcn_exp2f(sc[r]), p1 = __builtin_amdgcn_exp2f(sc[r + 1]);
+      ls0 = r ? ls0 + p0 : p0;
+      ls1 = r ? ls1 + p1 : p1;
+      pb[r >> 3][r & 7] = (f16)p0;
+      pb[r >> 3][(r & 7) + 1] = (f16)p1;
+    }
+    l_run += ls0 + ls1;
+    // O^T[dh][q] += V^T[dh][key] P^T[key][q]: two 32-row dh blocks x 2 key k-steps
+#pragma unroll
+    for (int db = 0; db < 2; ++db) {
+      const int vrow = db * 32 + l31;
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        const f16x8 vf = *reinterpret_cast<const f16x8*>(V_ + swz(vrow, 2 * (2 * kb2 + g) + hh));
+        acc[db] = mfma32(vf, pb[g], acc[db]);
+      }
+    }
+  };
+  using NF = std::false_type;
+  // the two blocks of tile kt, in order (a leading wave)
+  auto tile = [&](int kt, auto slot_tag, auto first_tag) {
+    constexpr int slot = decltype(slot_tag)::value;  // compile-time: LDS offsets fold into ds_read immediates
+    const char* K_ = smem + slot * SLOT;
+    softmax_pv(scores(K_, kt, 0, first_tag), K_ + TILE_B, 0, first_tag);
+    softmax_pv(scores(K_, kt, 1, NF{}), K_ + TILE_B, 1, NF{});
   };
 
   // tile kt lives in ring slot (kt - kt0) % R; the loop is unrolled over the
   // R slots so every LDS address is lane base + immediate.  Step kt issues
-  // tile kt+R-1 into the slot of tile kt-1 (released by the previous
+  // tile kt+DIST into the slot of tile kt-1 (released by the previous
   // barrier), computes tile kt, and waits -- counted, leaving the newer
   // tiles in flight -- for tile kt+1 before the barrier that ends the step.
   auto step = [&](int kt, auto slot_tag, auto first_tag) {
     constexpr int SL = decltype(slot_tag)::value;
-    if (kt + R - 1 < kt1) issue(kt + R - 1, (SL + R - 1) % R);
+    if (kt + DIST < kt1) issue(kt + DIST, (SL + DIST) % R);
     if (active) tile(kt, slot_tag, first_tag);
-    wait_tiles(min(kt1 - 1, kt + R - 1) - (kt + 1));
+    wait_tiles(min(kt1 - 1, kt + DIST) - (kt + 1));
     lds_barrier();
   };
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1 % R>;
   using S2 = std::integral_constant<int, 2 % R>;
   using S3 = std::integral_constant<int, 3 % R>;
-  using NF = std::false_type;
   step(kt0, S0{}, std::true_type{});
   int kt = kt0 + 1;
   for (; kt + R <= kt1; kt += R) {
