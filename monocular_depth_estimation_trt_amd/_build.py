@@ -79,6 +79,7 @@ def build_library(force: bool = False, verbose: bool = True, out: str = "", defi
     os.makedirs(objdir, exist_ok=True)
     dflags = [f"-D{d}" for d in defines]
     target = out or LIB
+    os.makedirs(os.path.dirname(os.path.abspath(target)), exist_ok=True)
 
     def compile_one(src: str) -> str:
         obj = os.path.join(objdir, src + ".o")

@@ -94,8 +94,12 @@ struct KGeo {
 #define MDE_GEMM_WPE_ATTR
 #endif
 
+// BK 32 (the short-K 128^2 dense stores): 3-stage ring = 48 KB and a half-size
+// epilogue staging, capped at 168 VGPRs -- three workgroups per CU, so one
+// workgroup's epilogue stores overlap the others' main loops
 template <int BM, int BN, int BK, int WM, int WN, int AM, int EM>
-__global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR gemm_kernel(const GemmParams p) {
+__global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
+    __attribute__((amdgpu_waves_per_eu(BK == 32 ? 3 : 1))) gemm_kernel(const GemmParams p) {
   using G = KGeo<BK>;
   constexpr int ROWB = G::ROWB, CH = G::CH;
   constexpr int NW = WM * WN;
@@ -111,7 +115,8 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR gemm_kernel(co
   constexpr int STAGE = (BM + BN) * ROWB;
   // dense A: SG-deep ring, every wave issues exactly NPER glds per stage so a
   // counted vmcnt names "stage kt has landed"
-  constexpr int SGMAX = 163840 / STAGE < MDE_GEMM_STAGES ? 163840 / STAGE : MDE_GEMM_STAGES;  // LDS limit
+  constexpr int SGWANT = BK == 32 ? 3 : MDE_GEMM_STAGES;
+  constexpr int SGMAX = 163840 / STAGE < SGWANT ? 163840 / STAGE : SGWANT;  // LDS limit
   constexpr int SG = (AM == A_DENSE && AINS % NW == 0 && BINS % NW == 0 && SGMAX > 2) ? SGMAX : 2;
   constexpr int NPER = APASS + BPASS;
   static_assert(SG >= 2 && SG <= 4, "stages");
@@ -455,27 +460,39 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR gemm_kernel(co
     if (z == z) return;
   }
 #endif
-  // LDS-staged epilogue when every wave's fp32 tile fits in the ring
-  constexpr bool EPI_LDS = MDE_EPI_LDS && BM * BN * 4 <= SG * STAGE;
+  // LDS-staged epilogue when every wave's fp32 tile fits in the ring, or
+  // (HALF) half of it: f16 rows / two fp32 row passes (store_tile_lds)
+  constexpr bool STG_FULL = BM * BN * 4 <= SG * STAGE;
+  constexpr int STG_HALF = !STG_FULL && BM * BN * 2 <= SG * STAGE;
+  constexpr bool EPI_LDS = MDE_EPI_LDS && (STG_FULL || STG_HALF);
   bool staged = false;
   if constexpr (EPI_LDS) {
     if constexpr (SG > 2) lds_barrier();  // the ring's last stage may still be read by other waves
     const int m0w = m0 + wm * TM * 16;
-    staged = store_tile_lds<EM, TM, TN>(
+    staged = store_tile_lds<EM, TM, TN, STG_HALF>(
         p, acc, [&](int row) { return m0w + row < p.M ? m0w + row : -1; }, n0 + wn * TN * 16, lane,
-        smem + wave * (TM * 16) * (TN * 16) * 4);
+        smem + wave * (TM * 16) * (TN * 16) * (STG_HALF ? 2 : 4));
   }
   if (!staged) store_tile<EM, TM, TN>(p, acc, mrow, n0 + wn * TN * 16 + (lane >> 4) * 4, lane);
 }
-template <int BM, int BN, int WM, int WN, int AM, int EM>
+template <int BM, int BN, int WM, int WN, int AM, int EM, int BKSEL = MDE_GEMM_BK>
 hipError_t run(const GemmParams& p, hipStream_t st) {
   const int gm = (p.M + BM - 1) / BM, gn = (p.N + BN - 1) / BN;
   const long long blocks = (long long)gm * gn;
   if (blocks <= 0) return hipSuccess;
-  constexpr int BKSEL = MDE_GEMM_BK;
   hipLaunchKernelGGL((gemm_kernel<BM, BN, BKSEL, WM, WN, AM, EM>), dim3((unsigned)blocks), dim3(WM * WN * 64), 0,
                      st, p);
   return hipGetLastError();
+}
+
+// dense 128^2 tiles on the BK 32 / 3-stage / three-per-CU kernel
+// (MDE_GEMM_BK32=0: the BK 64 two-stage kernel, A/B)
+bool bk32_tiles() {
+  static const int v = [] {
+    const char* e = getenv("MDE_GEMM_BK32");
+    return (e && e[0] == '0') ? 0 : 1;
+  }();
+  return v != 0;
 }
 
 // tuning override for large dense problems: MDE_GEMM_TILE = 256x256 | 256x128 | 128x256
@@ -487,6 +504,15 @@ int tile_override() {
     if (!strcmp(e, "256x128")) return 2;
     if (!strcmp(e, "128x256")) return 3;
     return 0;
+  }();
+  return v;
+}
+
+// 128^2 tiles once the grid holds at least this many of them (MDE_GEMM_BIG_MIN: tuning)
+long long big_tile_min() {
+  static const long long v = [] {
+    const char* e = getenv("MDE_GEMM_BIG_MIN");
+    return e ? atoll(e) : 240ll;
   }();
   return v;
 }
@@ -515,7 +541,17 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
       }
     }
     const long long big = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128);
-    if (big >= 240) return run<128, 128, 2, 2, AM, EM>(p, st);
+    if (big >= big_tile_min()) {
+      // short-K stores (ViT-S/B qkv, fc1: K 384 / 768 -> 6-12 K-steps, the
+      // epilogue a third of the launch) gain from the third workgroup per CU
+      // (B=28 ViT-S: fc1 1.30 -> 1.10 ms, qkv 0.97 -> 0.89 per forward); the
+      // residual updates (two fp32 staging passes) and K >= 1024 lose
+      // (fc2 0.85 -> 0.96, ViT-L B=8 qkv 2.56 -> 2.67)
+      if constexpr (AM == A_DENSE && (EM == E_STORE || EM == E_QKV)) {
+        if (p.K <= 768 && bk32_tiles()) return run<128, 128, 2, 2, AM, EM, 32>(p, st);
+      }
+      return run<128, 128, 2, 2, AM, EM>(p, st);
+    }
     return run<64, 64, 2, 2, AM, EM>(p, st);
   }
 }
