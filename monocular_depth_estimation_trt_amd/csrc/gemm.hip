@@ -487,6 +487,13 @@ hipError_t run(const GemmParams& p, hipStream_t st) {
 
 // dense 128^2 tiles on the BK 32 / 3-stage / three-per-CU kernel
 // (MDE_GEMM_BK32=0: the BK 64 two-stage kernel, A/B)
+int bk32_kmax() {  // MDE_GEMM_BK32_KMAX: tuning
+  static const int v = [] {
+    const char* e = getenv("MDE_GEMM_BK32_KMAX");
+    return e ? atoi(e) : 768;
+  }();
+  return v;
+}
 bool bk32_tiles() {
   static const int v = [] {
     const char* e = getenv("MDE_GEMM_BK32");
@@ -545,10 +552,11 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
       // short-K stores (ViT-S/B qkv, fc1: K 384 / 768 -> 6-12 K-steps, the
       // epilogue a third of the launch) gain from the third workgroup per CU
       // (B=28 ViT-S: fc1 1.30 -> 1.10 ms, qkv 0.97 -> 0.89 per forward); the
-      // residual updates (two fp32 staging passes) and K >= 1024 lose
-      // (fc2 0.85 -> 0.96, ViT-L B=8 qkv 2.56 -> 2.67)
+      // residual updates and K >= 1024 do not (fc2 0.85 -> 0.96 with two fp32
+      // staging passes, proj 0.43 -> 0.45 even with f16 staging of the
+      // update; ViT-L B=8 qkv 2.56 -> 2.67)
       if constexpr (AM == A_DENSE && (EM == E_STORE || EM == E_QKV)) {
-        if (p.K <= 768 && bk32_tiles()) return run<128, 128, 2, 2, AM, EM, 32>(p, st);
+        if (p.K <= bk32_kmax() && bk32_tiles()) return run<128, 128, 2, 2, AM, EM, 32>(p, st);
       }
       return run<128, 128, 2, 2, AM, EM>(p, st);
     }

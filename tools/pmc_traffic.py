@@ -51,7 +51,7 @@ def collect(root):
     return out
 
 
-HELPERS = ("splitk_resid_kernel",)   # second kernel of one engine step
+HELPERS = ("splitk_resid_kernel", "splitk_store_kernel", "attn_combine_kernel")  # second kernels of one engine step
 
 
 def per_pass_rows(root):
