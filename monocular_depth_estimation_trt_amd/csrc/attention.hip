@@ -39,8 +39,9 @@
 // sub-blocks per wave (256 VGPRs), 128-key tiles, one-block software
 // pipelining, an 8-wave ping-pong of MFMA / softmax segments and a lagged
 // second half (waves 4-7 half a tile behind, carrying the scores across the
-// barrier: 155 vs 113 us -- 226 VGPRs, one workgroup per CU) were all slower
-// than this form; 3- and 4-deep K/V rings (MDE_ATTN_CFG=8r3 / 8r4) measure
+// barrier: 155 vs 113 us at 226 VGPRs / one workgroup per CU, and 117-120 vs
+// 112-114 us with one loop per wave role at 128 VGPRs / two per CU) were all
+// slower than this form; 3- and 4-deep K/V rings (MDE_ATTN_CFG=8r3 / 8r4) measure
 // the same as 2 (SQ counters: the waits are issue/dependency stalls, not
 // load latency).
 #include <cstdlib>
