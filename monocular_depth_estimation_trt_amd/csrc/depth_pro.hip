@@ -176,6 +176,7 @@ size_t plan_arena_dp(const mde_engine& e, int B, DPBuf* b, uint8_t* base) {
     t.fv2 = a.h(bb * (GG / 4) * (F / 4));
     t.fv3 = a.h(bb * (GG / 16) * (F / 8));
   }
+  t.sws = a.f(kSplitWsFloats);
   if (b) *b = t;
   return a.off;
 }
@@ -284,6 +285,7 @@ hipError_t Runner::forward_dp(int B, const float* img, float* out, float* fov) {
   const int sd0 = cf.scaled_dims[0], sd1 = cf.scaled_dims[1], sd2 = cf.scaled_dims[2];
   const int id0 = cf.inter_dims[0], id1 = cf.inter_dims[1];
   const int ns = B * e.nseq;
+  split_ws = d.sws;
 
   // ---- encoders ----
   {

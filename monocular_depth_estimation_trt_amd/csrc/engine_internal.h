@@ -62,6 +62,7 @@ struct DPBuf {
   h16 *h0, *h1, *tb, *sb, *ub;     // fusion stage
   h16 *c1, *ct;                    // head
   h16 *fv1, *fv2, *fv3;            // fov head
+  float* sws;                      // E_STORE split-K partials (kSplitWsFloats)
 };
 
 // VGGT activations (vggt.hip plan_arena_vggt) over n = B*S frames.
@@ -76,6 +77,7 @@ struct VGBuf {
   h16 *tb, *sb, *ub, *vb, *p4, *p3, *p2, *c1;
   float* ws;               // fc2 split-K partials [4][ws_rows][D] (small-batch contexts only, else null)
   size_t ws_rows;
+  float* sws;              // E_STORE split-K partials (kSplitWsFloats)
 };
 
 enum Family : int { FAMILY_DAV2 = 0, FAMILY_DEPTH_PRO = 1, FAMILY_VGGT = 2 };

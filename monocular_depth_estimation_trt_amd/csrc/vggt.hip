@@ -168,6 +168,7 @@ size_t plan_arena_vggt(const mde_engine& e, int B, VGBuf* b, uint8_t* base) {
   t.c1 = a.h(n * s0 * (F / 2));
   t.ws_rows = n * T <= 4096 ? n * T : 0;
   t.ws = t.ws_rows ? a.f(4 * t.ws_rows * D) : nullptr;
+  t.sws = a.f(kSplitWsFloats);
   if (b) *b = t;
   return a.off;
 }
@@ -280,6 +281,7 @@ hipError_t Runner::forward_vggt(int B, const float* img, float* out) {
   const int D = e.D, T = e.T, np = e.np, F = e.F;
   const int* oc = cf.out_channels;
   char nm[64];
+  split_ws = v.sws;
 
   // ---- DINOv2-L/14-reg patch embedding over all frames ----
   step("patch_prep", [&] {

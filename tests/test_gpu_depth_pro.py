@@ -127,8 +127,15 @@ def test_graph_equals_eager_and_batch_consistency(tiny_case):
     yg, fg = run_engine(blob, x, graph=True)
     ye, fe = run_engine(blob, x, graph=False)
     assert np.array_equal(yg, ye) and np.array_equal(fg, fe)
-    y1, f1 = run_engine(blob, x[1:2])   # image 1 alone == image 1 of the batch
-    assert np.array_equal(y1[0], yg[1]) and np.array_equal(f1[0], fg[1])
+    # image 1 alone == image 1 of the batch, up to fp32 reassociation: the
+    # split-K slice count of the small-grid convs (gemm.hip
+    # store_split_slices) follows the grid, i.e. the batch
+    y1, f1 = run_engine(blob, x[1:2])
+    m = depth_metrics(y1[0:1], yg[1:2])
+    # (measured rel_mean 1.06e-3, corr 0.999999 on the tiny preset: the f16
+    # roundings downstream amplify the reassociation)
+    assert m["rel_mean"] < 3e-3 and m["max_abs"] <= 1e-2 * float(np.abs(yg[1]).max()), m
+    assert np.all(np.abs(f1[0] - fg[1]) <= 1e-3 * (1 + np.abs(fg[1]))), (f1, fg)
 
 
 def test_engine_real_widths_vs_hf_golden(gpu):
