@@ -659,9 +659,15 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
   if ((p.emode == E_RESID || p.emode == E_PATCH) && p.xh && ((uintptr_t)p.xh & 15)) return hipErrorInvalidValue;
   if (p.emode == E_RESID && p.splitk > 1 && p.partial && p.amode == A_DENSE) {
     // small M, long K (B = 1 fc2: 132 64^2 tiles x 24 K-steps): S slices of
-    // the K loop fill the chip, a second kernel adds them in slice order
+    // the K loop fill the chip, a second kernel adds them in slice order.
+    // When 128^2 tiles x 4 slices still give >= 320 workgroups (ViT-L /
+    // VGGT B = 1: 88 tiles), the 128^2 tiles halve the L2 -> LDS bytes per
+    // FLOP of the 64^2 ones; `partial` holds 4 slices (engine contract)
     const int nk = (p.K + 63) / 64;
-    int S = p.splitk < nk ? p.splitk : nk;
+    const long long t128 = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128);
+    const char* e128 = getenv("MDE_SPLITK128");
+    const bool big = t128 * 4 >= 320 && nk >= 16 && !(e128 && e128[0] == '0');
+    int S = big ? 4 : (p.splitk < nk ? p.splitk : nk);
     const int per = (nk + S - 1) / S;
     S = (nk + per - 1) / per;  // every slice non-empty
     GemmParams q = p;
@@ -671,9 +677,14 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
     q.bias = nullptr;
     q.ls = nullptr;
     q.lnst_out = nullptr;  // the reduce kernel writes the LN partials
-    const unsigned tiles = (unsigned)(((p.M + 63) / 64) * ((p.N + 63) / 64));
-    hipLaunchKernelGGL((gemm_kernel<64, 64, MDE_GEMM_BK, 2, 2, A_DENSE, E_PARTIAL>), dim3(tiles, (unsigned)S),
-                       dim3(256), 0, st, q);
+    if (big) {
+      hipLaunchKernelGGL((gemm_kernel<128, 128, MDE_GEMM_BK, 2, 2, A_DENSE, E_PARTIAL>), dim3((unsigned)t128, (unsigned)S),
+                         dim3(256), 0, st, q);
+    } else {
+      const unsigned tiles = (unsigned)(((p.M + 63) / 64) * ((p.N + 63) / 64));
+      hipLaunchKernelGGL((gemm_kernel<64, 64, MDE_GEMM_BK, 2, 2, A_DENSE, E_PARTIAL>), dim3(tiles, (unsigned)S),
+                         dim3(256), 0, st, q);
+    }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
     return launch_splitk_resid(p.partial, S, p.M, p.N, p.bias, p.ls, p.x32, p.xh, p.ldo, st, p.lnst_out);
