@@ -45,6 +45,9 @@
 #ifndef MDE_EPI_LDS
 #define MDE_EPI_LDS 1  // row-major epilogues staged through LDS (whole-line stores)
 #endif
+#ifndef MDE_BK32_STAGES
+#define MDE_BK32_STAGES 3  // ring depth of the BK 32 tiles (2: 33 KB, four workgroups per CU)
+#endif
 #ifndef MDE_GEMM_STAGES
 #define MDE_GEMM_STAGES 2  // LDS ring depth for dense A (>2: counted-vmcnt pipeline)
 #endif
@@ -99,7 +102,7 @@ struct KGeo {
 // workgroup's epilogue stores overlap the others' main loops
 template <int BM, int BN, int BK, int WM, int WN, int AM, int EM>
 __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
-    __attribute__((amdgpu_waves_per_eu(BK == 32 ? 3 : 1))) gemm_kernel(const GemmParams p) {
+    __attribute__((amdgpu_waves_per_eu(BK == 32 ? (MDE_BK32_STAGES > 2 ? 3 : 4) : 1))) gemm_kernel(const GemmParams p) {
   using G = KGeo<BK>;
   constexpr int ROWB = G::ROWB, CH = G::CH;
   constexpr int NW = WM * WN;
@@ -115,7 +118,7 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
   constexpr int STAGE = (BM + BN) * ROWB;
   // dense A: SG-deep ring, every wave issues exactly NPER glds per stage so a
   // counted vmcnt names "stage kt has landed"
-  constexpr int SGWANT = BK == 32 ? 3 : MDE_GEMM_STAGES;
+  constexpr int SGWANT = BK == 32 ? MDE_BK32_STAGES : MDE_GEMM_STAGES;
   constexpr int SGMAX = 163840 / STAGE < SGWANT ? 163840 / STAGE : SGWANT;  // LDS limit
   constexpr int SG = (AM == A_DENSE && AINS % NW == 0 && BINS % NW == 0 && SGMAX > 2) ? SGMAX : 2;
   constexpr int NPER = APASS + BPASS;
