@@ -551,6 +551,17 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
       }
     }
     const long long big = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128);
+    if constexpr (AM == A_DENSE && EM == E_RESID) {
+      // short-K residual updates (ViT-S proj, K 384) on 128 x 64 tiles: 48 KB
+      // LDS with full fp32 staging, three workgroups per CU (B=28: proj
+      // 0.427/0.431 -> 0.419/0.425 ms per forward, two same-box runs; fc2 at
+      // K 1536 loses, 0.86 -> 0.97).  MDE_RESID_N64_KMAX overrides the bound.
+      static const int kmax = [] {
+        const char* e = getenv("MDE_RESID_N64_KMAX");
+        return e ? atoi(e) : 384;
+      }();
+      if (p.K <= kmax && big >= big_tile_min()) return run<128, 64, 4, 1, AM, EM>(p, st);
+    }
     if (big >= big_tile_min()) {
       // short-K stores (ViT-S/B qkv, fc1: K 384 / 768 -> 6-12 K-steps, the
       // epilogue a third of the launch) gain from the third workgroup per CU
