@@ -623,7 +623,14 @@ int store_split_slices(const GemmParams& p) {
     const long long big = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128);
     wgs = big >= 240 ? big : t64;
   }
-  if (wgs >= 256 || nk < 8) return 1;
+  // at least 12 K-steps: the 64-channel convs of the ViT-S DPT (K 576, 9
+  // steps) run better unsplit (ViT-S B=1 0.925 -> 0.902 ms per forward with
+  // 12 vs 8; 16: 0.909); MDE_SPLIT_NKMIN overrides
+  static const int nkmin = [] {
+    const char* e = getenv("MDE_SPLIT_NKMIN");
+    return e ? atoi(e) : 12;
+  }();
+  if (wgs >= 256 || nk < nkmin) return 1;
   int S = (int)((512 + t64 - 1) / t64);
   S = S < nk / 4 ? S : nk / 4;  // >= 4 K-steps per slice
   S = S < 16 ? S : 16;
