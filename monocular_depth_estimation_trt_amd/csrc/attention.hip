@@ -121,11 +121,14 @@ struct SplitWs {
   int tiles = 0;        // key tiles per split
 };
 
-template <int NW, bool SPLIT, int R>
-__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4, 8)))
+template <int NW, bool SPLIT, int R, int QS = 1>
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(QS == 2 ? 2 : 4, 8)))
 attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16* __restrict__ vt,
                 f16* __restrict__ o, int H, int T, int Tpad, int ldo, SplitWs ws) {
-  constexpr int BQ = QW * NW;    // queries per workgroup
+  // QS = 2: each wave owns two 32-query sub-tiles; every K / V^T fragment
+  // read feeds both, and one sub-tile's softmax overlaps the other's MFMAs
+  static_assert(QS == 1 || (QS == 2 && !SPLIT), "query sub-tiles per wave");
+  constexpr int BQ = QW * NW * QS;  // queries per workgroup
   constexpr int INS = 8 / NW;    // glds instructions per wave per image (8 per 64-row image)
   constexpr int PER_TILE = 2 * INS;  // vmcnt entries one tile adds per wave (K + V^T)
   static_assert(NW == 4 || NW == 8, "waves per workgroup");
@@ -147,7 +150,7 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
   }
   const int bh = lin / nqb;
   const int b = bh / H, h = bh - (bh / H) * H;
-  const int qbase = (lin - bh * nqb) * BQ + wave * QW;
+  const int qbase = (lin - bh * nqb) * BQ + wave * QW * QS;
   const bool active = qbase < T;  // wave-uniform: a wave past the last query only helps load
   const int l31 = lane & 31, hh = lane >> 5;
 
@@ -162,11 +165,14 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
 
   // Q^T fragments (B operand), k-step s = dims 16s..16s+15: lane holds
   // Q[query][16s + 8hh + j] of its query column
-  const int qi = qbase + l31;
-  f16x8 qf[4];
+  const int qi = qbase + l31;  // sub-tile s: query qi + 32 s
+  f16x8 qf[QS][4];
 #pragma unroll
-  for (int st = 0; st < 4; ++st)
-    qf[st] = qi < Tpad ? *reinterpret_cast<const f16x8*>(qb + (size_t)qi * 64 + 16 * st + 8 * hh) : zero8();
+  for (int s = 0; s < QS; ++s)
+#pragma unroll
+    for (int st = 0; st < 4; ++st)
+      qf[s][st] = qi + 32 * s < Tpad ? *reinterpret_cast<const f16x8*>(qb + (size_t)(qi + 32 * s) * 64 + 16 * st + 8 * hh)
+                                     : zero8();
 
   // glds geometry: lane -> row lrow of an 8-row group, physical chunk lane & 7
   const int lrow = lane >> 3, pc = lane & 7;
@@ -185,13 +191,18 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
 
   // running max (log2 units) as an MFMA C operand: after the first block the
   // score MFMA computes S' = S - m_run directly in the accumulator
-  float m_run = 0.f, l_run = 0.f;
-  f32x16 negm, acc[2];
+  float m_run[QS], l_run[QS];
+  f32x16 negm[QS], acc[QS][2];
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    negm[r] = 0.f;
-    acc[0][r] = 0.f;
-    acc[1][r] = 0.f;
+  for (int s = 0; s < QS; ++s) {
+    m_run[s] = 0.f;
+    l_run[s] = 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      negm[s][r] = 0.f;
+      acc[s][0][r] = 0.f;
+      acc[s][1][r] = 0.f;
+    }
   }
 
   // wait until tile `kt` has landed, given the tiles issued after it: at
@@ -209,33 +220,44 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
   lds_barrier();
 
   // S'^T[key][query] = K Q^T - m_run over the 32 keys of block kb2 of tile
-  // kt (4 dim k-steps); keys >= T -> -inf
+  // kt (4 dim k-steps), for every query sub-tile (each K fragment read once);
+  // keys >= T -> -inf
+  struct Scores {
+    f32x16 v[QS];
+  };
   auto scores = [&](const char* K_, int kt, int kb2, auto first_tag) {
     constexpr bool FIRST = decltype(first_tag)::value;
-    f32x16 sc;
-    if constexpr (FIRST) {
+    Scores sc;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) sc[r] = 0.f;
-    } else {
-      sc = negm;
+    for (int s = 0; s < QS; ++s) {
+      if constexpr (FIRST) {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sc.v[s][r] = 0.f;
+      } else {
+        sc.v[s] = negm[s];
+      }
     }
     const int krow = kb2 * 32 + l31;
 #pragma unroll
     for (int st = 0; st < 4; ++st) {
       const f16x8 kf = *reinterpret_cast<const f16x8*>(K_ + swz(krow, 2 * st + hh));
-      sc = mfma32(kf, qf[st], sc);
+#pragma unroll
+      for (int s = 0; s < QS; ++s) sc.v[s] = mfma32(kf, qf[s][st], sc.v[s]);
     }
     if (kt * KT + kb2 * 32 + 32 > T) {  // last, partial block
       const int key0 = kt * KT + kb2 * 32 + 4 * hh;
 #pragma unroll
-      for (int r = 0; r < 16; ++r)
-        if (key0 + (r & 3) + 8 * (r >> 2) >= T) sc[r] = -INFINITY;
+      for (int s = 0; s < QS; ++s)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+          if (key0 + (r & 3) + 8 * (r >> 2) >= T) sc.v[s][r] = -INFINITY;
     }
     return sc;
   };
-  // online-softmax update and P.V of one block whose scores are sc (V_ = the
-  // V^T image of the block's tile)
-  auto softmax_pv = [&](f32x16 sc, const char* V_, int kb2, auto first_tag) {
+  // online-softmax update and P.V of sub-tile S whose scores are sc (V_ =
+  // the V^T image of the block's tile)
+  auto softmax_pv = [&](auto s_tag, f32x16 sc, const char* V_, int kb2, auto first_tag) {
+    constexpr int S = decltype(s_tag)::value;
     constexpr bool FIRST = decltype(first_tag)::value;
     // the lane's max over its 16 scores (v_max3 chain); the row max (partner
     // lane l ^ 32) only when some row rescales
@@ -246,15 +268,15 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
       mx = swap_max(mx);  // max of S' over the block (relative to m_run)
       // the running max grows by delta >= 0: shift S', rescale O and l
       const float delta = FIRST ? mx : fmaxf(mx, 0.f);
-      m_run += delta;
+      m_run[S] += delta;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) negm[r] = -m_run;
+      for (int r = 0; r < 16; ++r) negm[S][r] = -m_run[S];
       sc -= delta;
       if (!FIRST) {
         const float alpha = __builtin_amdgcn_exp2f(-delta);
-        l_run *= alpha;
-        acc[0] *= alpha;
-        acc[1] *= alpha;
+        l_run[S] *= alpha;
+        acc[S][0] *= alpha;
+        acc[S][1] *= alpha;
       }
     }
     // P = exp2(S'), row sums, and P^T as the PV B operand: registers
@@ -269,7 +291,7 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
       pb[r >> 3][r & 7] = (f16)p0;
       pb[r >> 3][(r & 7) + 1] = (f16)p1;
     }
-    l_run += ls0 + ls1;
+    l_run[S] += ls0 + ls1;
     // O^T[dh][q] += V^T[dh][key] P^T[key][q]: two 32-row dh blocks x 2 key k-steps
 #pragma unroll
     for (int db = 0; db < 2; ++db) {
@@ -277,17 +299,27 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
 #pragma unroll
       for (int g = 0; g < 2; ++g) {
         const f16x8 vf = *reinterpret_cast<const f16x8*>(V_ + swz(vrow, 2 * (2 * kb2 + g) + hh));
-        acc[db] = mfma32(vf, pb[g], acc[db]);
+        acc[S][db] = mfma32(vf, pb[g], acc[S][db]);
       }
     }
   };
   using NF = std::false_type;
-  // the two blocks of tile kt, in order (a leading wave)
+  // the two blocks of tile kt, in order
+  using Q0 = std::integral_constant<int, 0>;
+  using Q1 = std::integral_constant<int, QS - 1>;
   auto tile = [&](int kt, auto slot_tag, auto first_tag) {
     constexpr int slot = decltype(slot_tag)::value;  // compile-time: LDS offsets fold into ds_read immediates
     const char* K_ = smem + slot * SLOT;
-    softmax_pv(scores(K_, kt, 0, first_tag), K_ + TILE_B, 0, first_tag);
-    softmax_pv(scores(K_, kt, 1, NF{}), K_ + TILE_B, 1, NF{});
+    {
+      const Scores sc = scores(K_, kt, 0, first_tag);
+      softmax_pv(Q0{}, sc.v[0], K_ + TILE_B, 0, first_tag);
+      if constexpr (QS == 2) softmax_pv(Q1{}, sc.v[QS - 1], K_ + TILE_B, 0, first_tag);
+    }
+    {
+      const Scores sc = scores(K_, kt, 1, NF{});
+      softmax_pv(Q0{}, sc.v[0], K_ + TILE_B, 1, NF{});
+      if constexpr (QS == 2) softmax_pv(Q1{}, sc.v[QS - 1], K_ + TILE_B, 1, NF{});
+    }
   };
 
   // tile kt lives in ring slot (kt - kt0) % R; the loop is unrolled over the
@@ -321,7 +353,7 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
 
   if constexpr (SPLIT) {
     // unnormalised O^T (relative to m_run) and (m, l) of this key range
-    const float lt = swap_sum(l_run);
+    const float lt = swap_sum(l_run[0]);
     const size_t row = ((size_t)blockIdx.z * gridDim.y + bh) * ws.Tq + qi;
     float* orow = ws.o + row * 64;
 #pragma unroll
@@ -329,35 +361,40 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4)
         *reinterpret_cast<float4*>(orow + 32 * db + 8 * g4 + 4 * hh) =
-            make_float4(acc[db][4 * g4], acc[db][4 * g4 + 1], acc[db][4 * g4 + 2], acc[db][4 * g4 + 3]);
-    if (hh == 0) *reinterpret_cast<float2*>(ws.ml + row * 2) = make_float2(m_run, lt);
+            make_float4(acc[0][db][4 * g4], acc[0][db][4 * g4 + 1], acc[0][db][4 * g4 + 2], acc[0][db][4 * g4 + 3]);
+    if (hh == 0) *reinterpret_cast<float2*>(ws.ml + row * 2) = make_float2(m_run[0], lt);
     return;
   }
 
   // epilogue: lane holds O^T[dh = 32 db + (r&3) + 8(r>>2) + 4hh][qi]; pair
   // register groups (r>>2) = 2pr, 2pr+1 across the lane halves
   // (v_permlane32_swap) so each lane stores dh 16pr + 8hh .. +7 as one 16-B write
-  const float inv = 1.f / swap_sum(l_run);
-  uint4 out[2][2];
 #pragma unroll
-  for (int db = 0; db < 2; ++db)
-#pragma unroll
-    for (int pr = 0; pr < 2; ++pr) {
-      const int r0 = 8 * pr;  // group 2pr: registers r0..r0+3, group 2pr+1: r0+4..r0+7
-      const unsigned ax = pack2(acc[db][r0] * inv, acc[db][r0 + 1] * inv);
-      const unsigned ay = pack2(acc[db][r0 + 2] * inv, acc[db][r0 + 3] * inv);
-      const unsigned bx = pack2(acc[db][r0 + 4] * inv, acc[db][r0 + 5] * inv);
-      const unsigned by = pack2(acc[db][r0 + 6] * inv, acc[db][r0 + 7] * inv);
-      auto sx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
-      auto sy = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
-      out[db][pr] = make_uint4(sx[0], sy[0], sx[1], sy[1]);
-    }
-  if (qi < T) {
-    f16* orow = o + ((size_t)b * T + qi) * ldo + h * 64 + 8 * hh;
+  for (int sq = 0; sq < QS; ++sq) {
+    const float inv = 1.f / swap_sum(l_run[sq]);
+    uint4 out[2][2];
 #pragma unroll
     for (int db = 0; db < 2; ++db)
 #pragma unroll
-      for (int pr = 0; pr < 2; ++pr) *reinterpret_cast<uint4*>(orow + db * 32 + 16 * pr) = out[db][pr];
+      for (int pr = 0; pr < 2; ++pr) {
+        const int r0 = 8 * pr;  // group 2pr: registers r0..r0+3, group 2pr+1: r0+4..r0+7
+        const f32x16& a = acc[sq][db];
+        const unsigned ax = pack2(a[r0] * inv, a[r0 + 1] * inv);
+        const unsigned ay = pack2(a[r0 + 2] * inv, a[r0 + 3] * inv);
+        const unsigned bx = pack2(a[r0 + 4] * inv, a[r0 + 5] * inv);
+        const unsigned by = pack2(a[r0 + 6] * inv, a[r0 + 7] * inv);
+        auto sx = __builtin_amdgcn_permlane32_swap(ax, bx, false, false);
+        auto sy = __builtin_amdgcn_permlane32_swap(ay, by, false, false);
+        out[db][pr] = make_uint4(sx[0], sy[0], sx[1], sy[1]);
+      }
+    const int qs = qi + 32 * sq;
+    if (qs < T) {
+      f16* orow = o + ((size_t)b * T + qs) * ldo + h * 64 + 8 * hh;
+#pragma unroll
+      for (int db = 0; db < 2; ++db)
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) *reinterpret_cast<uint4*>(orow + db * 32 + 16 * pr) = out[db][pr];
+    }
   }
 }
 
@@ -398,16 +435,16 @@ __global__ void __launch_bounds__(256) attn_combine_kernel(SplitWs ws, int S, in
   *reinterpret_cast<f16x8*>(o + ((size_t)b * T + qi) * ldo + h * 64 + 8 * d8) = v;
 }
 
-template <int NW, int R>
+template <int NW, int R, int QS = 1>
 hipError_t run_attn(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T, int Tpad, int ldo,
                     float* ws, size_t ws_bytes, int split, hipStream_t st) {
-  constexpr int BQ = QW * NW;
+  constexpr int BQ = QW * NW * QS;
   const int nqb = (T + BQ - 1) / BQ, nkt = (T + KT - 1) / KT;
   const auto cq = reinterpret_cast<const f16*>(q);
   const auto ck = reinterpret_cast<const f16*>(k);
   const auto cv = reinterpret_cast<const f16*>(vt);
   const auto co = reinterpret_cast<f16*>(o);
-  if (split > 1 && ws) {
+  if (QS == 1 && split > 1 && ws) {
     SplitWs w;
     w.Tq = nqb * BQ;
     w.tiles = (nkt + split - 1) / split;
@@ -416,7 +453,7 @@ hipError_t run_attn(const h16* q, const h16* k, const h16* vt, h16* o, int B, in
     if (S > 1 && rows * 66 * sizeof(float) <= ws_bytes) {
       w.o = ws;
       w.ml = ws + rows * 64;
-      hipLaunchKernelGGL((attn_fwd_kernel<NW, true, R>), dim3(nqb, B * H, S), dim3(NW * 64), 0, st, cq, ck, cv, co, H, T,
+      hipLaunchKernelGGL((attn_fwd_kernel<NW, true, R, 1>), dim3(nqb, B * H, S), dim3(NW * 64), 0, st, cq, ck, cv, co, H, T,
                          Tpad, ldo, w);
       const hipError_t e = hipGetLastError();
       if (e != hipSuccess) return e;
@@ -426,7 +463,7 @@ hipError_t run_attn(const h16* q, const h16* k, const h16* vt, h16* o, int B, in
       return hipGetLastError();
     }
   }
-  hipLaunchKernelGGL((attn_fwd_kernel<NW, false, R>), dim3(nqb, B * H), dim3(NW * 64), 0, st, cq, ck, cv, co, H, T, Tpad,
+  hipLaunchKernelGGL((attn_fwd_kernel<NW, false, R, QS>), dim3(nqb, B * H), dim3(NW * 64), 0, st, cq, ck, cv, co, H, T, Tpad,
                      ldo, SplitWs{});
   return hipGetLastError();
 }
@@ -447,13 +484,14 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
   const int nkt = (T + KT - 1) / KT;
   // MDE_ATTN_CFG = <waves>[s<split>][r<ring>] ("8", "4", "4s8", "8r3", ...): tuning override
   static const char* forced = getenv("MDE_ATTN_CFG");
-  int nw = 0, split = 1, ring = ATTN_RING;
+  int nw = 0, split = 1, ring = ATTN_RING, qs2 = 0;
   if (forced) {
     nw = atoi(forced);
     const char* sp = strchr(forced, 's');
     split = sp ? atoi(sp + 1) : 1;
     const char* rp = strchr(forced, 'r');
     if (rp) ring = atoi(rp + 1);
+    qs2 = strstr(forced, "q2") != nullptr;
   }
   if (nw != 4 && nw != 8) {
     // 256-query workgroups share each K/V^T tile over 8 waves once the grid
@@ -468,6 +506,8 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
     if (nw == 4 && g128 < 256)
       while (split < 8 && nkt >= 7 * (split + 1) && g128 * (split + 1) <= 400) ++split;
   }
+  if (nw == 8 && qs2 && split <= 1) return run_attn<8, 2, 2>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, 1, st);
+  if (nw == 4 && qs2 && split <= 1) return run_attn<4, 2, 2>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, 1, st);
   if (nw == 8) {
     if (ring == 4) return run_attn<8, 4>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, split, st);
     if (ring == 3) return run_attn<8, 3>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, split, st);
