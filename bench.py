@@ -433,6 +433,10 @@ def main():
               "weights": wl.weights}
     if a.model == "vggt":
         config["frames"] = wl.frames
+        # oracle/vggt_ref.py: the aggregator (q/k norm, 2-D RoPE, frame/global
+        # alternation) is restated from the un-vendored upstream with nothing in
+        # the reference to pin it
+        config["parity"] = "partially pinned: aggregator parity unpinned"
     line = {
         "metric": f"depth FPS (images/s) at {S}x{S} fp16, {wl.label}, MI355X",
         "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
