@@ -1256,11 +1256,11 @@ int mde_op_patch_embed(const float* img, int batch, int h, int w, const void* wt
   OP_RET(launch_gemm(g, (hipStream_t)st), "patch_embed");
 }
 
-int mde_op_conv3x3(const void* in, int batch, int h, int w, int cin, const void* wt, int ldw, int cout, int stride,
-                   int relu_in, const float* bias, int act, const void* res0, const void* res1, void* out,
-                   void* st) {
-  if (!in || !wt || !out) return fail(MDE_ERR_ARG, "null argument");
-  if (stride != 1 && stride != 2) return fail(MDE_ERR_ARG, "stride must be 1 or 2");
+namespace {
+// GemmParams of a 3x3 / pad-1 conv over an NHWC f16 map (the mde_op_conv3x3* ops)
+GemmParams conv3x3_params(const void* in, int batch, int h, int w, int cin, const void* wt, int ldw, int cout,
+                          int stride, int relu_in, const float* bias, int act, const void* res0, const void* res1,
+                          void* out) {
   GemmParams g;
   g.amode = A_CONV3;
   g.A = (const h16*)in;
@@ -1283,6 +1283,16 @@ int mde_op_conv3x3(const void* in, int batch, int h, int w, int cin, const void*
   g.res1 = (const h16*)res1;
   g.out16 = (h16*)out;
   g.ldo = cout;
+  return g;
+}
+}  // namespace
+
+int mde_op_conv3x3(const void* in, int batch, int h, int w, int cin, const void* wt, int ldw, int cout, int stride,
+                   int relu_in, const float* bias, int act, const void* res0, const void* res1, void* out,
+                   void* st) {
+  if (!in || !wt || !out) return fail(MDE_ERR_ARG, "null argument");
+  if (stride != 1 && stride != 2) return fail(MDE_ERR_ARG, "stride must be 1 or 2");
+  const GemmParams g = conv3x3_params(in, batch, h, w, cin, wt, ldw, cout, stride, relu_in, bias, act, res0, res1, out);
   OP_RET(launch_gemm(g, (hipStream_t)st), "conv3x3");
 }
 
@@ -1291,28 +1301,7 @@ int mde_op_conv3x3_ws(const void* in, int batch, int h, int w, int cin, const vo
                       float* ws, size_t ws_floats, int* slices, void* st) {
   if (!in || !wt || !out || (!ws && ws_floats)) return fail(MDE_ERR_ARG, "null argument");
   if (stride != 1 && stride != 2) return fail(MDE_ERR_ARG, "stride must be 1 or 2");
-  GemmParams g;
-  g.amode = A_CONV3;
-  g.A = (const h16*)in;
-  g.cb = batch;
-  g.ch = h;
-  g.cw = w;
-  g.cc = cin;
-  g.stride = stride;
-  g.oh = (h - 1) / stride + 1;
-  g.ow = (w - 1) / stride + 1;
-  g.W = (const h16*)wt;
-  g.ldw = ldw;
-  g.M = batch * g.oh * g.ow;
-  g.N = cout;
-  g.K = 9 * cin;
-  g.relu_in = relu_in;
-  g.bias = bias;
-  g.act = act;
-  g.res0 = (const h16*)res0;
-  g.res1 = (const h16*)res1;
-  g.out16 = (h16*)out;
-  g.ldo = cout;
+  GemmParams g = conv3x3_params(in, batch, h, w, cin, wt, ldw, cout, stride, relu_in, bias, act, res0, res1, out);
   g.partial = ws;
   g.partial_cap = ws_floats;
   if (slices) *slices = gemm_store_split_slices(g);
