@@ -74,7 +74,7 @@ def parse(argv=None):
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--model", default="depth_anything_v2", choices=["depth_anything_v2", "depth_pro", "vggt"])
     p.add_argument("--batch", type=int, default=0,
-                   help="batch items per GPU per step (default 28; depth_pro 4; vggt 8)")
+                   help="batch items per GPU per step (default 48; depth_pro 4; vggt 8)")
     p.add_argument("--global-batch", type=int, default=0,
                    help="shard this many items over the ranks instead (strong scaling; config 3: 8)")
     p.add_argument("--frames", type=int, default=1, help="vggt: frames per batch item (the packed S)")
@@ -326,13 +326,14 @@ class Workload:
 
 
 DEFAULT_BATCH = {"depth_pro": 4, "vggt": 8,
-                 # B=28: attention runs 256-query workgroups (6 per head at T=1370),
-                 # 2 per CU -> 28 x 6 heads x 6 = 1008 workgroups = two full rounds
-                 # of 512 (B=30: 1080, a third round 11 % full: 122 vs 103 us per
-                 # launch, the same 4290 img/s overall); the N=384 GEMMs' 128^2
-                 # tiles also stay within whole rounds (B=32: 1029 for 1024 slots,
-                 # profiles/r01_v18_batch_sweep.json)
-                 "depth_anything_v2": 28}
+                 # B=48: with three workgroups per CU on the short-K GEMMs the
+                 # wave-quantisation tails of every kernel are what a larger
+                 # batch amortises -- same-box sweep with this round's kernels
+                 # (profiles/r02_v23_batch_sweep_24_48.txt, two passes each):
+                 # B=28 4843/4833, B=40 4886/4885, B=48 5015/4998 img/s; past 48
+                 # nothing more (r02_v23_batch_sweep_48_96.txt).  Round 1's B=28
+                 # (whole rounds of attention workgroups) no longer wins.
+                 "depth_anything_v2": 48}
 
 
 def rank_work(a, world, rank):
