@@ -86,4 +86,4 @@ def test_bench_rank_work():
     a = bench.parse(["--global-batch", "3"])
     assert [bench.rank_work(a, 4, r)[:2] for r in range(4)] == [(1, 0), (1, 1), (1, 2), (0, 3)]
     a = bench.parse([])
-    assert bench.rank_work(a, 4, 2)[:4] == (28, 56, 112, "weak")
+    assert bench.rank_work(a, 4, 2)[:4] == (48, 96, 192, "weak")  # default 48 per GPU
