@@ -37,8 +37,9 @@ Also measured (rank 0):
     (HBM-resident throughput); the like-for-like ratio is b1_vs_ref_fps
     (batch 1, PCIe-inclusive, the reference's method) and
     throughput_vs_ref_b1 = value / 232.11 says how far batching goes.
-  * cpu_baseline (N == 1 only): the oracle's fp32 CPU forward (a PyTorch
-    restatement of upstream DA-V2) on this host's cores, bounded sample.
+  * cpu_baseline (rank 0, after the timed region at every N): the oracle's
+    fp32 CPU forward (a PyTorch restatement of upstream DA-V2) on this host's
+    cores, bounded sample, in the same run (north_star).
 """
 
 from __future__ import annotations
@@ -55,7 +56,23 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-MFMA_PEAK_TFLOPS = 2500.0   # dense fp16/bf16 MFMA, MI355X (MI355X_MICROARCH.md chip table)
+MFMA_PEAK_TFLOPS = 2500.0   # dense fp16/bf16 MFMA, MI355X spec (MI355X_MICROARCH.md chip table)
+# measured on this chip (tools/mfma_peak.hip: back-to-back MFMAs on random f16
+# operands, every CU, clock settled): the sustained rate per MFMA shape --
+# attention runs 32x32x16, the GEMMs / convs 16x16x32
+MFMA_PEAK_FILE = os.path.join(ROOT, "profiles", "r03_mfma_peak.json")
+
+
+def measured_peak(kernel_class: str):
+    """(TFLOP/s, MFMA shape) the chip sustains for the instruction the class's
+    kernel issues, from the committed microbenchmark; (None, None) without it."""
+    try:
+        with open(MFMA_PEAK_FILE) as f:
+            d = json.load(f)
+    except (OSError, ValueError):
+        return None, None
+    shape = "32x32x16" if kernel_class.split(".")[-1] in ("attn", "attention", "gattn", "fattn") else "16x16x32"
+    return d.get(f"mfma_f16_{shape}_tflops"), shape
 ENC_LABEL = {"vits": "ViT-S", "vitb": "ViT-B", "vitl": "ViT-L"}
 REF_B1_FPS = 232.11         # RTX 3080 TRT fp16, BASELINE.md
 REF_B1_U8_FPS = 294.07      # same, uint8-NHWC input engine (reports/uint8_ab/depth_anything_v2.json)
@@ -159,6 +176,12 @@ def roofline(cfg, B, size, layer_ms, frames=1, traffic_file=""):
             "unit": "TFLOP/s", "frac": round(achieved / MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
             "flop_per_launch": per_launch_fl, "avg_launch_ms": round(avg_ms, 5),
             "launches_per_step": cls_n[dom]}
+    mp, shape = measured_peak(dom)
+    if mp:
+        roof.update({"peak_source": "spec (MI355X_MICROARCH.md)", "peak_measured": mp,
+                     "peak_measured_mfma": f"v_mfma_f32_{shape}_f16",
+                     "peak_measured_source": os.path.relpath(MFMA_PEAK_FILE, ROOT),
+                     "frac_of_measured": round(achieved / mp, 4)})
     if traffic is not None:
         roof["traffic_unit"] = "bytes/launch"
         roof["traffic_source"] = os.path.relpath(traffic_file, ROOT)
@@ -411,6 +434,10 @@ def main():
     layer_ms = profile_layers(ctx, sh, a.profile_iters)
     tfile = traffic_path(a.model, wl.encoder, B, S, wl.frames)
     roof, breakdown = roofline(wl.cfg, B, S, layer_ms, wl.frames, tfile)
+    if roof["traffic"] is None:
+        log(f"no committed PMC profile covers '{roof['kernel']}' at this workload "
+            f"({os.path.relpath(tfile, ROOT)}): roofline.traffic is null -- "
+            f"bash tools/profile_round.sh <out> {' '.join(sys.argv[1:])}")
     if a.layers_json:
         with open(a.layers_json, "w") as f:
             json.dump({"batch": B, "frames": wl.frames, "layer_ms": layer_ms, "classes": breakdown, "roofline": roof},
@@ -425,7 +452,8 @@ def main():
         res_b1["b1_model_mfma_frac"] = round(wl.gflop * 1e9 / (res_b1["b1_compute_ms"] * 1e-3) /
                                              (MFMA_PEAK_TFLOPS * 1e12), 4)
     cpu = None
-    if world == 1 and not a.no_cpu_baseline:
+    if not a.no_cpu_baseline:
+        # N > 1: the other ranks are done and wait at the closing barrier
         cpu = cpu_baseline(wl.cfg, S, a.cpu_seconds)
     for c, v in list(breakdown.items())[:10]:
         log(f"{c:24s} {v['ms']:9.4f} ms  x{v['launches']:3d}  {v['tflops']} TF/s")

@@ -765,6 +765,7 @@ int mde_context_destroy(mde_context* c) {
     hipGraphExecDestroy(kv.second.second);
     hipGraphDestroy(kv.second.first);
   }
+  for (auto& kv : c->graph_done) hipEventDestroy(kv.second);
   for (auto& pe : c->prof_events) {
     hipEventDestroy(pe.second.first);
     hipEventDestroy(pe.second.second);
@@ -880,11 +881,17 @@ int mde_context_enqueue(mde_context* c, void* stream) {
   auto it = c->graphs.find(key);
   if (it == c->graphs.end() && (int)c->graphs.size() >= mde_context::kMaxGraphs) {
     // evict the least recently launched graph; its last replay may still be
-    // running on some caller stream, so drain the device first (rare path)
-    HIP_OR(hipDeviceSynchronize(), "hipDeviceSynchronize (graph eviction)");
+    // running on some caller stream: wait for that replay's event only (no
+    // device-wide sync, which would also break a caller capturing its stream)
     auto lru = c->graph_used.begin();
     for (auto u = c->graph_used.begin(); u != c->graph_used.end(); ++u)
       if (u->second < lru->second) lru = u;
+    auto done = c->graph_done.find(lru->first);
+    if (done != c->graph_done.end()) {
+      HIP_OR(hipEventSynchronize(done->second), "hipEventSynchronize (graph eviction)");
+      hipEventDestroy(done->second);
+      c->graph_done.erase(done);
+    }
     auto victim = c->graphs.find(lru->first);
     hipGraphExecDestroy(victim->second.second);
     hipGraphDestroy(victim->second.first);
@@ -912,6 +919,9 @@ int mde_context_enqueue(mde_context* c, void* stream) {
   }
   c->graph_used[key] = ++c->graph_tick;
   HIP_OR(hipGraphLaunch(it->second.second, st), "hipGraphLaunch");
+  hipEvent_t& ev = c->graph_done[key];
+  if (!ev) HIP_OR(hipEventCreateWithFlags(&ev, hipEventDisableTiming), "hipEventCreate");
+  HIP_OR(hipEventRecord(ev, st), "hipEventRecord");
   return MDE_OK;
 }
 

@@ -146,6 +146,9 @@ struct mde_context {
   static constexpr int kMaxGraphs = 8;
   std::map<mde::GraphKey, std::pair<hipGraph_t, hipGraphExec_t>> graphs;
   std::map<mde::GraphKey, unsigned long long> graph_used;
+  // per cached graph: an event recorded behind its latest replay, so an
+  // eviction waits for that replay only (not the whole device)
+  std::map<mde::GraphKey, hipEvent_t> graph_done;
   unsigned long long graph_tick = 0;
   mde_layer_cb prof_cb = nullptr;
   void* prof_user = nullptr;

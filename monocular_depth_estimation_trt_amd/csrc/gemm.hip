@@ -332,17 +332,7 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
   float4 c1v[TN];  // lnc1 of this lane's columns (an epilogue load would cost every tile an L2 round trip)
   auto ln_partial_loads = [&] {
     if constexpr (LNF) {
-#ifdef MDE_FOLD_EXP  // timing experiment: no partial / c1 loads (wrong results)
       if (p.lnst_in) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) c1v[j] = float4{0.f, 0.f, 0.f, 0.f};
-        for (int r = tid; r < BM; r += NT)
-          *reinterpret_cast<float2*>(smem + SG * STAGE + r * 8) = make_float2(0.f, 1.f);
-      }
-      if (false) {
-#else
-      if (p.lnst_in) {
-#endif
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int n = n0 + wn * TN * 16 + j * 16 + (lane >> 4) * 4;
@@ -621,7 +611,7 @@ int store_split_slices(const GemmParams& p) {
     wgs = (long long)p.cb * ((p.oh + 7) / 8) * ((p.ow + 15) / 16) * ((p.N + bn - 1) / bn);
   } else {
     const long long big = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128);
-    wgs = big >= 240 ? big : t64;
+    wgs = big >= big_tile_min() ? big : t64;
   }
   // at least 12 K-steps: the 64-channel convs of the ViT-S DPT (K 576, 9
   // steps) run better unsplit (ViT-S B=1 0.925 -> 0.902 ms per forward with
@@ -712,7 +702,9 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
   }
   if (p.lnst_out || p.lnst_in) {
     // folded LayerNorm: the 128^2 / 64^2 kernels of this file (partials per
-    // 32-column slice from the LDS-staged epilogue, the fold after the main loop)
+    // 32-column slice from the LDS-staged epilogue, the fold after the main loop;
+    // a tile that falls back to the direct epilogue writes NaN partials)
+    if (p.lnst_out && !MDE_EPI_LDS) return hipErrorInvalidValue;
     if ((p.lnst_ns * 32 != (p.lnst_out ? p.N : p.K)) ||
         (p.lnst_in && (p.lnst_ns > 32 || (p.lnst_ns & 3) || p.lnst_rows != p.M)) ||
         (p.lnst_out && p.lnst_rows < (p.emode == E_PATCH ? p.M / p.npatch * p.T : p.M)) || (p.lnst_in && (!p.lnc1 || p.amode != A_DENSE)) ||

@@ -18,6 +18,13 @@ MDE_DEV size_t res0_offset(const GemmParams& p, int m, int n, size_t o) {
   return p.res0_rows > 0 ? (size_t)(m % p.res0_rows) * p.ldo + n : o;
 }
 
+// NaN (sum, M2) for the 32-column slice of column n in row `row` of the
+// folded-LayerNorm partials (GemmParams::lnst_out)
+MDE_DEV void poison_ln_partials(const GemmParams& p, int row, int n) {
+  *reinterpret_cast<float2*>(p.lnst_out + ((size_t)(n >> 5) * p.lnst_rows + row) * 2) =
+      make_float2(__builtin_nanf(""), __builtin_nanf(""));
+}
+
 template <int EM, int TM, int TN>
 MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&mrow)[TM], int ncol, int lane) {
   if constexpr (EM == E_HEAD) {
@@ -126,6 +133,11 @@ MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&m
             *reinterpret_cast<f16x4*>(dst) = h;
           }
         } else if constexpr (EM == E_RESID) {
+          // the folded-LayerNorm partials are written by the LDS-staged
+          // epilogue only (whole 32-column slices per wave): a tile that
+          // reaches this direct path poisons them, so the next qkv / fc1
+          // produces NaN instead of silently normalising with stale stats
+          if (p.lnst_out) poison_ln_partials(p, m, n);
           const float4 l = *reinterpret_cast<const float4*>(p.ls + n);
           if (p.xh) {  // f16 residual stream: fp32 update, one rounding
             f16x4* x = reinterpret_cast<f16x4*>(reinterpret_cast<f16*>(p.xh) + (size_t)m * p.ldo + n);
@@ -148,6 +160,7 @@ MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&m
           const int b = m / p.npatch, pi = m - (m / p.npatch) * p.npatch;
           const float4 ps = *reinterpret_cast<const float4*>(p.pos + (size_t)pi * p.ldo + n);
           const size_t xo = ((size_t)b * p.T + p.tok0 + pi) * p.ldo + n;
+          if (p.lnst_out) poison_ln_partials(p, (int)((size_t)b * p.T + p.tok0 + pi), n);
           if (p.xh) {
             f16x4 h = {(f16)(v[0] + ps.x), (f16)(v[1] + ps.y), (f16)(v[2] + ps.z), (f16)(v[3] + ps.w)};
             *reinterpret_cast<f16x4*>(reinterpret_cast<f16*>(p.xh) + xo) = h;

@@ -21,6 +21,10 @@ full-map statistics, plus the FOV scalars.
                                  decoder 256, scaled dims 1024/1024/512) with 4
                                  blocks per encoder; output every 2nd pixel in
                                  f16 (768x768) + full-map statistics
+  depth_pro_full_b1.npz          B=1, use_fov=True, the full "dinov2l16_384"
+                                 preset (24 blocks per encoder, hooks [11, 5]):
+                                 the bench model itself; output every 2nd
+                                 pixel in f16 + full-map statistics + FOV
 """
 
 from __future__ import annotations
@@ -93,6 +97,7 @@ def run_case(name, preset, batch, use_fov=True, seed=4321, first_seed=200, sub=8
 CASES = {
     "depth_pro_tiny_b2": dict(preset="tiny", batch=2),
     "depth_pro_shallow_b1": dict(preset="dinov2l16_384_shallow", batch=1, first_seed=300, sub=2, f16=True),
+    "depth_pro_full_b1": dict(preset="dinov2l16_384", batch=1, first_seed=400, sub=2, f16=True),
 }
 
 if __name__ == "__main__":

@@ -106,10 +106,12 @@ def test_engine_matches_oracle(tiny_case):
     m = depth_metrics(y, ref)
     print("depth_pro tiny B=2", m, "fov", fov, fov_ref)
     assert np.isfinite(y).all() and np.isfinite(fov).all()
-    assert m["rel_mean"] <= 1e-2, m
-    assert m["corr"] >= 0.999, m
-    assert m["max_abs"] <= 0.03 * float(np.abs(ref).max()), m
-    assert np.all(np.abs(fov - fov_ref) <= 2e-2 + 1e-2 * np.abs(fov_ref)), (fov, fov_ref)
+    # ~3x the measured error (profiles/r02_gpu_tests.log: rel 1.41e-3,
+    # max_abs 0.0152, corr 0.9999985, fov |d| 6.6e-4)
+    assert m["rel_mean"] <= 4e-3, m
+    assert m["corr"] >= 0.99999, m
+    assert m["max_abs"] <= 0.045, m
+    assert np.all(np.abs(fov - fov_ref) <= 2e-3), (fov, fov_ref)
 
 
 def test_engine_matches_hf_golden(tiny_case):
@@ -118,8 +120,8 @@ def test_engine_matches_hf_golden(tiny_case):
     assert WD.state_dict_digest(sd) == str(z["weights_sha256"])
     y, fov = run_engine(blob, x)
     m = depth_metrics(y[:, ::8, ::8], z["output_hf_sub8"])
-    assert m["rel_mean"] <= 1e-2 and m["corr"] >= 0.999, m
-    assert np.all(np.abs(fov - z["fov_hf"]) <= 2e-2 + 1e-2 * np.abs(z["fov_hf"])), (fov, z["fov_hf"])
+    assert m["rel_mean"] <= 4e-3 and m["corr"] >= 0.99999 and m["max_abs"] <= 0.045, m
+    assert np.all(np.abs(fov - z["fov_hf"]) <= 2e-3), (fov, z["fov_hf"])
 
 
 def test_graph_equals_eager_and_batch_consistency(tiny_case):
@@ -138,12 +140,8 @@ def test_graph_equals_eager_and_batch_consistency(tiny_case):
     assert np.all(np.abs(f1[0] - fg[1]) <= 1e-3 * (1 + np.abs(fg[1]))), (f1, fg)
 
 
-def test_engine_real_widths_vs_hf_golden(gpu):
-    """Depth Pro at its real widths (D 1024 / 16 heads / decoder 256 / scaled
-    dims 1024-1024-512, the "dinov2l16_384_shallow" preset: 4 blocks per
-    encoder), B=1 at 1536^2, canonical inverse depth + fov_deg, against the
-    HF golden (every 2nd pixel, f16).  Same bars as the tiny preset."""
-    z = np.load(os.path.join(GOLDEN, "depth_pro_shallow_b1.npz"), allow_pickle=False)
+def _real_width_case(golden, rel, max_abs, fov_tol):
+    z = np.load(os.path.join(GOLDEN, golden), allow_pickle=False)
     cfg = WD.depth_pro_config(str(z["preset"]))
     sd = WD.synthetic_state_dict(cfg, int(z["seed"]))
     assert WD.state_dict_digest(sd) == str(z["weights_sha256"])
@@ -151,13 +149,31 @@ def test_engine_real_widths_vs_hf_golden(gpu):
     y, fov = run_engine(pack_depth_pro.pack_bytes(sd, cfg), x)
     ref = z["output_hf_sub2_f16"].astype(np.float32)
     m = depth_metrics(y[:, ::2, ::2], ref)
-    print("depth_pro real widths B=1", m, "fov", fov, z["fov_hf"], "full mean", float(y.mean()), float(z["out_mean"]))
+    print(f"depth_pro {z['preset']} B=1", m, "fov", fov, z["fov_hf"], "full mean", float(y.mean()),
+          float(z["out_mean"]), "ref max", float(np.abs(ref).max()))
     assert np.isfinite(y).all() and np.isfinite(fov).all()
-    assert m["rel_mean"] <= 1e-2, m
-    assert m["corr"] >= 0.999, m
-    assert m["max_abs"] <= 0.03 * float(np.abs(ref).max()), m
-    assert abs(float(y.mean()) - float(z["out_mean"])) <= 1e-2 * abs(float(z["out_mean"]))
-    assert np.all(np.abs(fov - z["fov_hf"]) <= 2e-2 + 1e-2 * np.abs(z["fov_hf"])), (fov, z["fov_hf"])
+    assert m["rel_mean"] <= rel, m
+    assert m["corr"] >= 0.99999, m
+    assert m["max_abs"] <= max_abs, m
+    assert abs(float(y.mean()) - float(z["out_mean"])) <= rel * abs(float(z["out_mean"]))
+    assert np.all(np.abs(fov - z["fov_hf"]) <= fov_tol), (fov, z["fov_hf"])
+
+
+def test_engine_real_widths_vs_hf_golden(gpu):
+    """Depth Pro at its real widths (D 1024 / 16 heads / decoder 256 / scaled
+    dims 1024-1024-512, the "dinov2l16_384_shallow" preset: 4 blocks per
+    encoder), B=1 at 1536^2, canonical inverse depth + fov_deg, against the
+    HF golden (every 2nd pixel, f16).  Bars ~3x the measured error
+    (profiles/r02_gpu_tests.log: rel 6.3e-4, max_abs 0.016, fov |d| 2.3e-5)."""
+    _real_width_case("depth_pro_shallow_b1.npz", rel=2e-3, max_abs=0.05, fov_tol=1e-3)
+
+
+def test_engine_full_depth_vs_hf_golden(gpu):
+    """The bench model itself: the full "dinov2l16_384" preset (24 blocks per
+    encoder, hooks [11, 5] -- the tap indexing at real depth), B=1 at 1536^2,
+    against its HF golden (tests/golden/make_golden_depth_pro.py
+    depth_pro_full_b1; models/depth_pro/onnx_export.py:13-28)."""
+    _real_width_case("depth_pro_full_b1.npz", rel=2e-3, max_abs=0.05, fov_tol=1e-3)
 
 
 def test_engine_rejects_bad_shapes(tiny_case):

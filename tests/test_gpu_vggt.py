@@ -67,25 +67,30 @@ def tiny_s2(gpu):
     return _case("tiny", 1, 2)
 
 
-def _check(y, ref, what):
+# Tolerances: about 3x the error measured on MI355X (profiles/r02_gpu_tests.log:
+# tiny B=2 rel 6.6e-4 / max_abs 0.0037, tiny S=2 7.1e-4 / 0.0061, VGGT-1B
+# widths at 518^2 9.3e-4 / 0.0055, corr >= 0.999997 everywhere), so a
+# numerical regression of a few x fails.  Against the oracle only: the VGGT
+# aggregator is parity-unpinned.
+def _check(y, ref, what, rel=2e-3, max_abs=0.02):
     m = depth_metrics(y, ref)
     print(what, m, "ref range", float(ref.min()), float(ref.max()))
     assert y.shape == ref.shape, (y.shape, ref.shape)
     assert np.isfinite(y).all()
-    assert m["rel_mean"] <= 1e-2, m
-    assert m["corr"] >= 0.999, m
-    assert m["max_abs"] <= 0.03 * float(np.abs(ref).max()), m
+    assert m["rel_mean"] <= rel, m
+    assert m["corr"] >= 0.99999, m
+    assert m["max_abs"] <= max_abs, m
 
 
 def test_tiny_batch2_matches_oracle(tiny_b2):
     cfg, sd, x, ref, blob = tiny_b2
-    _check(run_engine(blob, x), ref, "vggt tiny B=2 S=1")
+    _check(run_engine(blob, x), ref, "vggt tiny B=2 S=1", rel=2e-3, max_abs=0.012)
 
 
 def test_tiny_two_frames_matches_oracle(tiny_s2):
     """S = 2: global attention over both frames, special-token set 1 on frame 1."""
     cfg, sd, x, ref, blob = tiny_s2
-    _check(run_engine(blob, x), ref, "vggt tiny B=1 S=2")
+    _check(run_engine(blob, x), ref, "vggt tiny B=1 S=2", rel=2e-3, max_abs=0.02)
 
 
 def test_graph_equals_eager_and_batch_consistency(tiny_b2):
@@ -100,7 +105,7 @@ def test_graph_equals_eager_and_batch_consistency(tiny_b2):
 def test_vggt_1b_shallow_518_matches_oracle(gpu):
     cfg, sd, x, ref, blob = _case("vggt_1b_shallow", 1, 1)
     assert ref.shape == (1, 1, 518, 518, 1)
-    _check(run_engine(blob, x), ref, "vggt_1b_shallow 518 B=1")
+    _check(run_engine(blob, x), ref, "vggt_1b_shallow 518 B=1", rel=3e-3, max_abs=0.017)
 
 
 def test_engine_rejects_bad_shapes(tiny_b2):
