@@ -62,6 +62,15 @@ MDE_DEV void ac_index(float scale, int dst, int in_size, int& i0, int& i1, float
 // 0..3}; stored at 16g + 8h + 0..7 they are one contiguous 16-byte read.
 MDE_DEV int vt_pos(int t) { return (t & ~12) | ((t & 4) << 1) | ((t & 8) >> 1); }
 
+// XCD-aware workgroup order (bijective for any grid): workgroups are dealt
+// round-robin over the 8 XCDs (bid % 8 shares an L2), so renumber them to
+// give each XCD a contiguous run -- neighbouring work items that share
+// source lines then fetch them into one L2 instead of several.
+MDE_DEV int xcd_remap(int bid, int nwg) {
+  const int q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
+  return (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
+}
+
 // Tile (tm, tn) of the linear workgroup index `bid` (after the XCD remap,
 // which hands each XCD a contiguous run of bids).  gm <= 1: row-major, N
 // fastest -- the N tiles of a row block share A in one L2.  gm > 1: row

@@ -328,26 +328,31 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
       for (int it = 0; it < 4; ++it) {
         const int r0 = shift + 4 * (it * 4 + (lane >> 4));
         int mm[4], be[4], te[4];
-        f32x4 rows[4];
+        f16x4 rows[4];  // the staged values are f16 outputs either way: 8 VGPRs, not 16
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const bool in = r0 + e < R;
           mm[e] = in ? mof(r0 + e) : -1;
           be[e] = b0 + (r0 + e >= rb ? 1 : 0);
           te[e] = t00 + r0 + e - (r0 + e >= rb ? p.T : 0);
-          rows[e] = in ? rd4(f16_tag, r0 + e, dc) : f32x4{0.f, 0.f, 0.f, 0.f};
+          if constexpr (decltype(f16_tag)::value) {
+            rows[e] = in ? *reinterpret_cast<const f16x4*>(lds + phys8(r0 + e, dc)) : f16x4{};
+          } else {
+            const f32x4 v = in ? rd4(f16_tag, r0 + e, dc) : f32x4{0.f, 0.f, 0.f, 0.f};
+            rows[e] = f16x4{(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+          }
         }
         const bool quad = mm[0] >= 0 && mm[3] >= 0 && (te[0] & 3) == 0 && be[3] == be[0];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           f16* col = vt0 + (size_t)(4 * dc + k) * p.Tpad;
           if (quad) {
-            f16x4 h = {(f16)rows[0][k], (f16)rows[1][k], (f16)rows[2][k], (f16)rows[3][k]};
+            f16x4 h = {rows[0][k], rows[1][k], rows[2][k], rows[3][k]};
             *reinterpret_cast<f16x4*>(col + be[0] * hs + vt_pos(te[0])) = h;
           } else {
 #pragma unroll
             for (int e = 0; e < 4; ++e)
-              if (mm[e] >= 0) col[be[e] * hs + vt_pos(te[e])] = (f16)rows[e][k];
+              if (mm[e] >= 0) col[be[e] * hs + vt_pos(te[e])] = rows[e][k];
           }
         }
       }

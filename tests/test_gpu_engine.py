@@ -90,7 +90,8 @@ def test_engine_vs_golden_98(gpu, name):
 @pytest.mark.parametrize("name,encoder", [("dav2_vits_metric_518", "vits"), ("dav2_vitl_metric_518", "vitl")])
 def test_engine_vs_golden_518(gpu, name, encoder):
     """Full 518x518 map at B=1 against HF.  ViT-L at B=1 is BASELINE config
-    3's per-GPU unit: its fc2 runs as 2 split-K slices (engine.hip split_k)."""
+    3's per-GPU unit: its fc2 runs split-K, 128^2 tiles x 4 slices of the K loop
+    (gemm.hip launch_gemm, E_RESID split), reduced in slice order."""
     z = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
     cfg = weights.model_config(encoder, "metric")
     sd = weights.synthetic_state_dict(cfg, int(z["seed"]))

@@ -21,6 +21,10 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--lib", default="")
     ap.add_argument("--only", default="")
+    ap.add_argument("--dim", type=int, default=384, help="ViT width D (ViT-L: 1024)")
+    ap.add_argument("--heads", type=int, default=6, help="attention heads (ViT-L: 16)")
+    ap.add_argument("--cold", action="store_true",
+                    help="also time each launch alone after a 512 MB write (caches cold, as in the graph)")
     a = ap.parse_args()
     if a.lib:
         os.environ["MDE_LIB"] = a.lib
@@ -28,7 +32,7 @@ def main():
     from gpu_util import conv_w, pad_w, ptr, stream
     from monocular_depth_estimation_trt_amd import _lib
     dev = torch.device("cuda:0")
-    B, T, D, H = a.batch, 1370, 384, 6
+    B, T, D, H = a.batch, 1370, a.dim, a.heads
     M = B * T
     g = torch.Generator(device=dev).manual_seed(0)
 
@@ -48,21 +52,34 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / a.iters
-        print(f"{name:28s} {ms * 1e3:9.1f} us  {flop / ms / 1e9:8.1f} TF/s", flush=True)
+        line = f"{name:28s} {ms * 1e3:9.1f} us  {flop / ms / 1e9:8.1f} TF/s"
+        if a.cold:
+            cold = []
+            for _ in range(max(5, a.iters // 4)):
+                flush.fill_(1.0)
+                e0.record()
+                fn()
+                e1.record()
+                torch.cuda.synchronize()
+                cold.append(e0.elapsed_time(e1))
+            cms = sorted(cold)[len(cold) // 2]
+            line += f"   cold {cms * 1e3:9.1f} us  {flop / cms / 1e9:8.1f} TF/s"
+        print(line, flush=True)
 
     L = _lib.lib()
     st = stream()
+    flush = torch.empty(128 << 20, device=dev) if a.cold else None  # 512 MB > L2 + Infinity Cache
     x16 = rnd(M, 4 * D)
     out = torch.empty(M, 4 * D, dtype=torch.float16, device=dev)
     x32 = torch.randn(M, D, device=dev)
     bias = torch.randn(4 * D, device=dev) * 0.02
     ls = torch.full((4 * D,), 0.5, device=dev)
-    for name, n, k, act in (("qkv-like N1152 K384", 3 * D, D, 0), ("fc1 N1536 K384 gelu", 4 * D, D, 2),
-                            ("fc1 N1536 K384 nogelu", 4 * D, D, 0)):
+    for name, n, k, act in ((f"qkv-like N{3 * D} K{D}", 3 * D, D, 0), (f"fc1 N{4 * D} K{D} gelu", 4 * D, D, 2),
+                            (f"fc1 N{4 * D} K{D} nogelu", 4 * D, D, 0)):
         w = pad_w(rnd(n, k, scale=k ** -0.5))
         timeit(name, lambda: L.mde_op_linear(ptr(x16), k, ptr(w), w.shape[1], M, n, k, ptr(bias), act, ptr(out),
                                              n, st), 2.0 * M * n * k)
-    for name, n, k in (("proj N384 K384 resid", D, D), ("fc2 N384 K1536 resid", D, 4 * D)):
+    for name, n, k in ((f"proj N{D} K{D} resid", D, D), (f"fc2 N{D} K{4 * D} resid", D, 4 * D)):
         w = pad_w(rnd(n, k, scale=k ** -0.5))
         timeit(name, lambda: L.mde_op_linear_residual(ptr(x16), k, ptr(w), w.shape[1], M, n, k, ptr(bias), ptr(ls),
                                                       ptr(x32), D, st), 2.0 * M * n * k)
@@ -71,7 +88,7 @@ def main():
     q = torch.zeros(B * H, Tp, 64, dtype=torch.float16, device=dev)
     k_ = torch.zeros_like(q)
     vt = torch.zeros(B * H, 64, Tp, dtype=torch.float16, device=dev)
-    timeit("qkv N1152 K384 (E_QKV)", lambda: L.mde_op_qkv(ptr(x16), ptr(w), w.shape[1], ptr(bias), B, T, H, Tp,
+    timeit(f"qkv N{3 * D} K{D} (E_QKV)", lambda: L.mde_op_qkv(ptr(x16), ptr(w), w.shape[1], ptr(bias), B, T, H, Tp,
                                                         0.125, ptr(q), ptr(k_), ptr(vt), st), 2.0 * M * 3 * D * D)
     # the engine's operands: q pre-scaled by dh^-0.5 * log2(e) (E_QKV), so
     # scores are O(1) in log2 units -- unscaled N(0,1) q and k would put the
@@ -80,7 +97,7 @@ def main():
     k_.normal_()
     vt.normal_()
     o = torch.empty(M, D, dtype=torch.float16, device=dev)
-    timeit("attention T1370 H6", lambda: L.mde_op_attention(ptr(q), ptr(k_), ptr(vt), ptr(o), B, H, T, Tp, D, st),
+    timeit(f"attention T1370 H{H}", lambda: L.mde_op_attention(ptr(q), ptr(k_), ptr(vt), ptr(o), B, H, T, Tp, D, st),
            4.0 * B * H * T * T * 64)
     F = 64
     for hw in (148, 74):
