@@ -144,10 +144,7 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
   // not eight (PMC: 4.5x the algorithmic bytes without it).  Bijective.
   const int nqb = gridDim.x, nwg = gridDim.x * gridDim.y;
   int lin = blockIdx.y * nqb + blockIdx.x;
-  {
-    const int q8 = nwg / 8, r8 = nwg % 8, x = lin % 8;
-    lin = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + lin / 8;
-  }
+  lin = xcd_remap(lin, nwg);
   const int bh = lin / nqb;
   const int b = bh / H, h = bh - (bh / H) * H;
   const int qbase = (lin - bh * nqb) * BQ + wave * QW * QS;

@@ -114,11 +114,7 @@ __global__ void __launch_bounds__(WM * WN * 64) conv3_kernel(const GemmParams p)
   // vertically adjacent tiles then share their halo / bilinear source rows in
   // one L2 instead of each XCD fetching them again (head.output_conv2 at
   // B=30 fetched ~2x its 168 MB source map without it).  Bijective.
-  int bid = blockIdx.x;
-  {
-    const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
-    bid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
-  }
+  int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int tn = bid % ntn;
   bid /= ntn;
   const int tx = bid % tiles_x;

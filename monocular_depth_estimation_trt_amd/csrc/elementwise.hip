@@ -9,12 +9,6 @@
 #include "mde_device.h"
 #include "mde_ops.h"
 
-#ifdef MDE_ELEM_NOREMAP  // A/B: round-robin block order for resize / patch_prep
-#define ELEM_BLOCK(b, n) (b)
-#else
-#define ELEM_BLOCK(b, n) xcd_remap(b, n)
-#endif
-
 namespace mde {
 
 namespace {
@@ -134,9 +128,9 @@ __global__ void __launch_bounds__(256) patch_prep_kernel(const float* __restrict
                                                          const float* __restrict__ cls_st) {
   const long long np = (long long)ph * pw;
   const long long nchunk = (long long)B * np * 84;  // 3 channels x 14 rows x 2 halves
-  // XCD-contiguous block order: horizontally adjacent patches share the
-  // 128-B lines of their 56-B row spans
-  long long id = (long long)ELEM_BLOCK(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  // round-robin block order (see resize_kernel: the XCD-contiguous order
+  // reads exactly the input, 269 -> 155 MB, but takes 62.9 -> 68.4 us)
+  long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (id < nchunk) {
     long long patch;
     int r, b, pi;
@@ -194,7 +188,7 @@ __global__ void __launch_bounds__(256) patch_prep_u8_kernel(const unsigned char*
                                                             const float* __restrict__ cls_st) {
   const long long np = (long long)ph * pw;
   const long long nchunk = (long long)B * np * 28;  // 14 rows x 2 halves
-  long long id = (long long)ELEM_BLOCK(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (id < nchunk) {
     const long long patch = id / 28;
     const int r = (int)(id - patch * 28);
@@ -271,10 +265,13 @@ __global__ void __launch_bounds__(256) resize_kernel(const f16* __restrict__ in,
                                                      int ih, int iw, int C, int oh, int ow) {
   const int C8 = C >> 3;
   const long long n = (long long)B * oh * ow * C8;
-  // XCD-contiguous block order: the 2-4 output rows that blend from one
-  // source row stay on one XCD (round-robin order fetched each source row
-  // into up to 8 L2s: rf2.resize 150 MB fetched for a 34 MB source at B=48)
-  const long long id = (long long)ELEM_BLOCK(blockIdx.x, gridDim.x) * blockDim.x + threadIdx.x;
+  // Block order stays round-robin over the XCDs: an XCD-contiguous order
+  // (mde_device.h xcd_remap) fetches each source row into one L2 only (rf2
+  // at B=48: 150 -> 34 MB fetched, = the source map) but runs SLOWER, 44.9
+  // -> 54-56 us (profiles/r03_v2_remap_ab.txt); the duplicate fetches are
+  // Infinity-Cache hits, and one address-ordered stream over the whole map
+  // beats eight disjoint ones
+  const long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (id >= n) return;
   int c8, ox, oy, b;
   if (n < (1LL << 31)) {  // 32-bit index split: a 64-bit divide is a long emulated sequence

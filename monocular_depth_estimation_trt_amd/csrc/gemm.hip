@@ -137,10 +137,7 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
   // (tn fastest) -- the N-tiles of one row block then share A in one L2.
   // Bijective for any grid size (cdna_hip_programming.md section 5).
   int bid = blockIdx.x;
-  if (MDE_XCD_REMAP) {
-    const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
-    bid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
-  }
+  if (MDE_XCD_REMAP) bid = xcd_remap(bid, gridDim.x);
   int tm, tn;
   tile_of(bid, (p.M + BM - 1) / BM, ntn, AM == A_DENSE ? tile_group_m(p.N, p.K, BM) : 1, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;

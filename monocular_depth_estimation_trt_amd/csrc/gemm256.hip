@@ -72,11 +72,7 @@ __global__ void __launch_bounds__(NW * 64) gemm256_kernel(const GemmParams p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wave >> 2, wc = wave & 3;
   const int ntn = (p.N + BN - 1) / BN;
-  int bid = blockIdx.x;
-  {  // XCD-aware order (bijective): each XCD takes a contiguous run, N fastest
-    const int nwg = gridDim.x, q8 = nwg / 8, r8 = nwg % 8, x = bid % 8;
-    bid = (x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8) + bid / 8;
-  }
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);  // XCD-aware order: each XCD a contiguous run, N fastest
   int tm, tn;
   tile_of(bid, (p.M + BM - 1) / BM, ntn, tile_group_m(p.N, p.K, BM), tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;

@@ -1,0 +1,89 @@
+"""Build ablation variants of libmde_hip.so without touching the product source.
+
+    python tools/ablate.py NAME            -> build/var/lib_NAME.so
+
+Each variant copies csrc/ to build/ablate/NAME/, applies text substitutions
+to one kernel file (asserting each pattern is present) and links a library
+with the product flags.  The variants answer "where does this kernel's time
+go" (cdna_hip_programming.md section 5.4 rule 17: keep stubbed values live
+with an empty asm so the compiler cannot delete the work upstream of them);
+their outputs are wrong by construction and they are timing tools only
+(tools/bench_kernels.py --lib build/var/lib_NAME.so).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+# name -> (file, [(old, new, count)])
+VARIANTS = {
+    # attention: the softmax exponentials replaced by their argument
+    "attn_noexp": ("attention.hip", [
+        ("const float p0 = __builtin_amdgcn_exp2f(sc[r]), p1 = __builtin_amdgcn_exp2f(sc[r + 1]);",
+         "const float p0 = sc[r], p1 = sc[r + 1];", 1)]),
+    # attention: no P.V MFMAs (P and the V fragments kept live)
+    "attn_nopv": ("attention.hip", [
+        ("acc[S][db] = mfma32(vf, pb[g], acc[S][db]);",
+         'asm volatile("" :: "v"(vf), "v"(pb[g]));', 1)]),
+    # attention: no score MFMAs (K fragments kept live, scores = C operand)
+    "attn_noqk": ("attention.hip", [
+        ("for (int s = 0; s < QS; ++s) sc.v[s] = mfma32(kf, qf[s][st], sc.v[s]);",
+         'for (int s = 0; s < QS; ++s) asm volatile("" :: "v"(kf), "v"(qf[s][st]));', 1)]),
+    # attention: no K/V waits or barriers (LDS races: wrong values, timing only)
+    "attn_nosync": ("attention.hip", [
+        ("""MDE_DEV void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}""", """MDE_DEV void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+}""", 1),
+        ("""MDE_DEV void wait_vm_n() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}""", """MDE_DEV void wait_vm_n() {
+}""", 1)]),
+}
+
+
+def build(name: str) -> str:
+    from monocular_depth_estimation_trt_amd import _build
+    fname, subs = VARIANTS[name]
+    work = os.path.join(ROOT, "build", "ablate", name)
+    if os.path.exists(work):
+        shutil.rmtree(work)
+    shutil.copytree(_build.CSRC, work)
+    path = os.path.join(work, fname)
+    with open(path) as f:
+        s = f.read()
+    for old, new, count in subs:
+        n = s.count(old)
+        if n != count:
+            raise SystemExit(f"{name}: pattern found {n} times (expected {count}): {old[:60]!r}")
+        s = s.replace(old, new)
+    with open(path, "w") as f:
+        f.write(s)
+    out = os.path.join(ROOT, "build", "var", f"lib_{name}.so")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    # only the edited file is recompiled (against the product headers); the
+    # other objects are the product build's (build/obj, `_build.build_library`)
+    _build.build_library()
+    cc = _build.hipcc()
+    obj = os.path.join(work, fname + ".o")
+    cmd = [cc, *_build.FLAGS, *_build.PER_FILE.get(fname, []), "-c", path, "-o", obj]
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode:
+        raise SystemExit(f"{name}: hipcc failed\n{r.stderr[-3000:]}")
+    objs = [obj if src == fname else os.path.join(_build.OBJDIR, src + ".o") for src in _build.SOURCES]
+    subprocess.run([cc, f"--offload-arch={_build.ARCH}", "-shared", "-fPIC", "-o", out, *objs], check=True)
+    print(f"[ablate] built {out}")
+    return out
+
+
+if __name__ == "__main__":
+    for n in sys.argv[1:] or sorted(VARIANTS):
+        build(n)
