@@ -440,16 +440,6 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
     const int m = m0 + wm * TM * 16 + i * 16 + (lane & 15);
     mrow[i] = m < p.M ? m : -1;
   }
-#ifdef MDE_EXP_NOEPI  // tuning experiment: main loop only (stores only if a NaN appears)
-  {
-    float z = 0.f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) z += acc[i][j][0] + acc[i][j][3];
-    if (z == z) return;
-  }
-#endif
   // LDS-staged epilogue when every wave's fp32 tile fits in the ring, or
   // (HALF) half of it: f16 rows / two fp32 row passes (store_tile_lds)
   constexpr bool STG_FULL = BM * BN * 4 <= SG * STAGE;

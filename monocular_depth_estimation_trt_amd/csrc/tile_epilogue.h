@@ -89,11 +89,7 @@ MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&m
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
           }
-#ifdef MDE_EXP_STORE_SMALL  // tuning experiment: same stores, L2-resident target rows
-          const size_t o = (size_t)(m & 255) * p.ldo + n;
-#else
           const size_t o = (size_t)m * p.ldo + n;
-#endif
           if (p.res0) {
             const f16x4 r0 =
                 *reinterpret_cast<const f16x4*>(reinterpret_cast<const f16*>(p.res0) + res0_offset(p, m, n, o));
@@ -277,10 +273,8 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
 #pragma unroll
               for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
             } else if (p.act == ACT_GELU) {
-#ifndef MDE_EXP_NOGELU  // timing experiment: GELU skipped (wrong results)
 #pragma unroll
               for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
-#endif
             }
           }
           const int row = (i - PS * (TM / NP)) * 16 + (lane & 15);

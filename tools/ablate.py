@@ -47,6 +47,23 @@ VARIANTS = {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }""", """MDE_DEV void wait_vm_n() {
 }""", 1)]),
+    # GEMM main loop only: the epilogue returns unless a NaN appears (r02's
+    # MDE_EXP_NOEPI, profiles/r02_v10_epilogue_cost_*)
+    "gemm_noepi": ("gemm.hip", [
+        ("""  // LDS-staged epilogue when every wave's fp32 tile fits in the ring, or""",
+         """  {
+    float z = 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) z += acc[i][j][0] + acc[i][j][3];
+    if (z == z) return;
+  }
+  // LDS-staged epilogue when every wave's fp32 tile fits in the ring, or""", 1)]),
+    # GEMM: no MFMAs in the main loop (fragments kept live): the load / sync skeleton alone
+    "gemm_nomfma": ("gemm.hip", [
+        ("for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);",
+         'for (int j = 0; j < TN; ++j) asm volatile("" :: "v"(fb[j]), "v"(fa[i]));', 1)]),
 }
 
 

@@ -84,6 +84,74 @@ def census(insts):
     return cls, valu
 
 
+def analyse(insts):
+    """Census dict of one kernel's instruction list (kernels()[name])."""
+    addr_idx = {ad: i for i, (ad, _, _) in enumerate(insts)}
+    # loops: backward branches (objdump prints the target as <kernel+0xoff>)
+    loops = []
+    for i, (ad, mn, ops) in enumerate(insts):
+        if mn.startswith("s_cbranch") or mn == "s_branch":
+            m = re.search(r"<[^+>]+\+0x([0-9a-f]+)>", ops)
+            if m:
+                j = addr_idx.get(insts[0][0] + int(m.group(1), 16))
+                if j is not None and j < i:
+                    loops.append((i - j, j, i))
+    loops.sort(reverse=True)
+    res = {"total_insts": len(insts)}
+    tot_cls, _ = census(insts)
+    res["kernel_classes"] = dict(tot_cls)
+    if not loops:
+        return res
+    n, j, i = loops[0]
+    body = insts[j:i + 1]
+    cls, valu = census(body)
+    # forward branches inside the body: the skipped ranges are conditional code
+    cond = []
+    for k, (ad, mn, ops) in enumerate(body):
+        if mn.startswith("s_cbranch"):
+            m = re.search(r"<[^+>]+\+0x([0-9a-f]+)>", ops)
+            if m:
+                tgt = insts[0][0] + int(m.group(1), 16)
+                if ad < tgt <= body[-1][0]:
+                    kk = next(x for x in range(k, len(body)) if body[x][0] >= tgt)
+                    cond.append({"from": hex(ad), "to": hex(tgt), "insts": kk - k - 1,
+                                 "classes": dict(census(body[k + 1:kk])[0])})
+    nm = cls["mfma"]
+    v_all = cls["valu"] + cls["valu_trans"] + cls["valu_accmov"]
+    res["loop"] = {"insts": len(body), "start": hex(body[0][0]), "end": hex(body[-1][0]),
+                   "classes": dict(cls), "valu_by_mnemonic": dict(valu.most_common()),
+                   "valu_per_mfma_static": round(v_all / nm, 2) if nm else None,
+                   "conditional_ranges": cond}
+    # hot path: the loop body minus the forward-skipped ranges that hold no
+    # MFMA -- the last-block key mask and the online-softmax rescale, taken
+    # on a few blocks per row (ranges WITH MFMAs, e.g. "wave active", run)
+    skip = set()
+    for c in cond:
+        if c["classes"].get("mfma", 0) == 0:
+            lo, hi = int(c["from"], 16), int(c["to"], 16)
+            skip.update(k for k, (ad, _, _) in enumerate(body) if lo < ad < hi)
+    # the first branch back to the loop head closes the hot iteration (the
+    # code after it, up to the final back-edge, is a rare tail: the last
+    # block's rescale falls through there)
+    head = body[0][0]
+    first_back = len(body) - 1
+    for k, (ad, mn, ops) in enumerate(body):
+        if mn.startswith("s_cbranch") or mn == "s_branch":
+            m = re.search(r"<[^+>]+\+0x([0-9a-f]+)>", ops)
+            if m and insts[0][0] + int(m.group(1), 16) == head:
+                first_back = k
+                break
+    hot = [x for k, x in enumerate(body) if k not in skip and k <= first_back]
+    hcls, hvalu = census(hot)
+    hv = hcls["valu"] + hcls["valu_trans"] + hcls["valu_accmov"]
+    if nm:
+        res["hot_path"] = {"insts": len(hot), "classes": dict(hcls), "valu_by_mnemonic": dict(hvalu.most_common()),
+                           "valu_per_mfma": round(hv / nm, 2),
+                           "trans_per_mfma": round(hcls["valu_trans"] / nm, 2),
+                           "salu_per_mfma": round(hcls["salu"] / nm, 2)}
+    return res
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--src", default=os.path.join(ROOT, "monocular_depth_estimation_trt_amd", "csrc", "attention.hip"))
@@ -92,67 +160,7 @@ def main():
     a = ap.parse_args()
     ks = kernels(disassemble(a.src))
     name = next(k for k in ks if a.kernel in k)
-    insts = ks[name]
-    addr_idx = {ad: i for i, (ad, _, _) in enumerate(insts)}
-    # loops: backward branches; target encoded as "label" address in the operand text
-    loops = []
-    for i, (ad, mn, ops) in enumerate(insts):
-        if mn.startswith("s_cbranch") or mn == "s_branch":
-            m = re.search(r"<[^+>]+\+0x([0-9a-f]+)>", ops)
-            if m:
-                # objdump prints <kernel+0xoff>: offset from the symbol start
-                j = addr_idx.get(insts[0][0] + int(m.group(1), 16))
-                if j is not None and j < i:
-                    loops.append((i - j, j, i))
-    loops.sort(reverse=True)
-    res = {"kernel": name, "total_insts": len(insts)}
-    tot_cls, _ = census(insts)
-    res["kernel_classes"] = dict(tot_cls)
-    if loops:
-        n, j, i = loops[0]
-        body = insts[j:i + 1]
-        cls, valu = census(body)
-        # forward branches inside the body: the skipped ranges are conditional code
-        cond = []
-        for k, (ad, mn, ops) in enumerate(body):
-            if mn.startswith("s_cbranch"):
-                m = re.search(r"<[^+>]+\+0x([0-9a-f]+)>", ops)
-                if m:
-                    tgt = insts[0][0] + int(m.group(1), 16)
-                    if tgt > ad and tgt <= body[-1][0]:
-                        kk = next(x for x in range(k, len(body)) if body[x][0] >= tgt)
-                        cond.append({"from": hex(ad), "to": hex(tgt), "insts": kk - k - 1,
-                                     "classes": dict(census(body[k + 1:kk])[0])})
-        nm = cls["mfma"]
-        v_all = cls["valu"] + cls["valu_trans"] + cls["valu_accmov"]
-        res["loop"] = {"insts": len(body), "start": hex(body[0][0]), "end": hex(body[-1][0]),
-                       "classes": dict(cls), "valu_by_mnemonic": dict(valu.most_common()),
-                       "valu_per_mfma_static": round(v_all / nm, 2) if nm else None,
-                       "conditional_ranges": cond}
-        # hot path: the loop body minus the forward-skipped ranges that hold no
-        # MFMA -- the last-block key mask and the online-softmax rescale, taken
-        # on a few blocks per row (ranges WITH MFMAs, e.g. "wave active", run)
-        skip = set()
-        for c in cond:
-            if c["classes"].get("mfma", 0) == 0:
-                lo, hi = int(c["from"], 16), int(c["to"], 16)
-                skip.update(k for k, (ad, _, _) in enumerate(body) if lo < ad < hi)
-        # the first branch back to the loop head closes the hot iteration (the
-        # code after it, up to the final back-edge, is a rare tail: the last
-        # block's rescale falls through there)
-        head = body[0][0]
-        first_back = next((k for k, (ad, mn, ops) in enumerate(body)
-                           if (mn.startswith("s_cbranch") or mn == "s_branch")
-                           and (m := re.search(r"<[^+>]+\+0x([0-9a-f]+)>", ops))
-                           and insts[0][0] + int(m.group(1), 16) == head), len(body) - 1)
-        hot = [x for k, x in enumerate(body) if k not in skip and k <= first_back]
-        hcls, hvalu = census(hot)
-        hv = hcls["valu"] + hcls["valu_trans"] + hcls["valu_accmov"]
-        if nm:
-            res["hot_path"] = {"insts": len(hot), "classes": dict(hcls), "valu_by_mnemonic": dict(hvalu.most_common()),
-                               "valu_per_mfma": round(hv / nm, 2),
-                               "trans_per_mfma": round(hcls["valu_trans"] / nm, 2),
-                               "salu_per_mfma": round(hcls["salu"] / nm, 2)}
+    res = {"kernel": name, **analyse(ks[name])}
     out = json.dumps(res, indent=1)
     if a.json:
         with open(a.json, "w") as f:
