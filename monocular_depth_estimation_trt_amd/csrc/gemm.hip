@@ -102,7 +102,8 @@ struct KGeo {
 // workgroup's epilogue stores overlap the others' main loops
 template <int BM, int BN, int BK, int WM, int WN, int AM, int EM>
 __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
-    __attribute__((amdgpu_waves_per_eu(BK == 32 ? (MDE_BK32_STAGES > 2 ? 3 : 4) : 1))) gemm_kernel(const GemmParams p) {
+    __attribute__((amdgpu_waves_per_eu(BK == 32 ? (WM * WN == 8 ? 4 : (MDE_BK32_STAGES > 2 ? 3 : 4)) : 1)))
+    gemm_kernel(const GemmParams p) {
   using G = KGeo<BK>;
   constexpr int ROWB = G::ROWB, CH = G::CH;
   constexpr int NW = WM * WN;
@@ -490,6 +491,7 @@ int tile_override() {
     if (!strcmp(e, "256x256")) return 1;
     if (!strcmp(e, "256x128")) return 2;
     if (!strcmp(e, "128x256")) return 3;
+    if (!strcmp(e, "256x128w8")) return 4;  // 8 waves, BK 32 x 3 stages, two workgroups per CU
     return 0;
   }();
   return v;
@@ -517,6 +519,11 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
       }
     }
   }
+  if constexpr (AM == A_DENSE && EM != E_HEAD) {
+    // 256 x 128 tiles on 8 waves (4 x 2 of 64 x 64), BK 32 x 3 stages = 72 KB:
+    // two workgroups per CU, 25 % fewer L2 -> LDS bytes per FLOP than 128^2
+    if (tile_override() == 4 && p.M >= 256 && p.N >= 128) return run<256, 128, 4, 2, AM, EM, 32>(p, st);
+  }
   if constexpr (EM == E_HEAD) {
     return run<128, 32, 4, 1, AM, EM>(p, st);
   } else {
@@ -529,6 +536,18 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
     }
     const long long big = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128);
     if constexpr (AM == A_DENSE && EM == E_RESID) {
+      // residual updates with at least two rounds of 256 x 128 tiles (8 waves,
+      // BK 32 x 3 stages, two workgroups per CU): 25 % fewer L2 -> LDS bytes per
+      // FLOP and twice the rows per workgroup for the read-modify-write
+      // epilogue.  ViT-S B = 48, same box, two passes: proj 0.685 / 0.690 ->
+      // 0.611 / 0.606 ms, fc2 1.493 / 1.503 -> 1.401 / 1.394 ms per forward,
+      // qkv / fc1 unchanged on this tile (profiles/r03_v3_*).  MDE_RESID_W8=0: off
+      static const bool w8 = [] {
+        const char* e = getenv("MDE_RESID_W8");
+        return !(e && e[0] == '0');
+      }();
+      const long long t256 = (long long)((p.M + 255) / 256) * ((p.N + 127) / 128);
+      if (w8 && t256 >= 512) return run<256, 128, 4, 2, AM, EM, 32>(p, st);
       // short-K residual updates (ViT-S proj, K 384) on 128 x 64 tiles: 48 KB
       // LDS with full fp32 staging, three workgroups per CU (B=28: proj
       // 0.427/0.431 -> 0.419/0.425 ms per forward, two same-box runs; fc2 at

@@ -391,18 +391,55 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
       constexpr int PS = decltype(ps_tag)::value, NP = decltype(np_tag)::value;
       constexpr bool F16 = decltype(f16_tag)::value;
       constexpr int RP = R / NP;  // rows staged per pass
+      // f16 staging of a mode whose staged value IS the output (E_STORE without
+      // residuals -- f16stage -- E_QKV with the q scale applied in park, E_CONVT):
+      // the row leaves as the staged 16 bytes, no f16 -> f32 -> f16 round trip
+      constexpr bool RAW = F16 && (EM == E_STORE || EM == E_QKV || EM == E_CONVT);
       if (n >= p.N) return;
+      // E_QKV: (image, token) of this lane's rows, advanced by RPI rows per
+      // iteration instead of a 32-bit division per row (GEMM row maps are
+      // linear: m = m0 + row)
+      int qb = 0, qt = 0;
+      if constexpr (EM == E_QKV) {
+        const int m0r = mof(PS * RP + rr);
+        if (m0r < 0) return;
+        qb = m0r / p.T;
+        qt = m0r - qb * p.T;
+      }
 #pragma unroll
       for (int it = 0; it < (RP + RPI - 1) / RPI; ++it) {
         const int row = it * RPI + rr;
         if (RP % RPI != 0 && row >= RP) break;
+        if constexpr (EM == E_QKV) {
+          if (it > 0) {
+            qt += RPI;
+            while (qt >= p.T) {
+              qt -= p.T;
+              ++qb;
+            }
+          }
+        }
         const int m = mof(PS * RP + row);
         if (m < 0) continue;
-        const f32x4 a = rd4(f16_tag, row, 2 * cc);
-        const f32x4 b = rd4(f16_tag, row, 2 * cc + 1);
-        float v[8] = {a[0], a[1], a[2], a[3], b[0], b[1], b[2], b[3]};
+        f16x8 raw{};
+        float v[8];
+        if constexpr (RAW) {
+          raw = *reinterpret_cast<const f16x8*>(lds + phys8(row, 2 * cc));
+        } else {
+          const f32x4 a = rd4(f16_tag, row, 2 * cc);
+          const f32x4 b = rd4(f16_tag, row, 2 * cc + 1);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) {
+            v[r] = a[r];
+            v[4 + r] = b[r];
+          }
+        }
         if constexpr (EM == E_STORE) {
           const size_t o = (size_t)m * p.ldo + n;
+          if constexpr (RAW) {
+            *reinterpret_cast<f16x8*>(reinterpret_cast<f16*>(p.out16) + o) = raw;
+            continue;
+          }
           if (p.res0) {
             const f16x8 r0 =
                 *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res0) + res0_offset(p, m, n, o));
@@ -466,20 +503,24 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
           const int y = rem / p.iw, x = rem - (rem / p.iw) * p.iw;
           const int OH = p.ih * p.s, OW = p.iw * p.s;
           const size_t o = (((size_t)b * OH + y * p.s + dy) * OW + x * p.s + dx) * p.ldo + co;
-          f16x8 h;
+          f16x8 h = raw;
+          if constexpr (!RAW) {
 #pragma unroll
-          for (int r = 0; r < 8; ++r) h[r] = (f16)v[r];
+            for (int r = 0; r < 8; ++r) h[r] = (f16)v[r];
+          }
           *reinterpret_cast<f16x8*>(reinterpret_cast<f16*>(p.out16) + o) = h;
         } else {  // E_QKV, q or k third
           const int D = p.heads * 64, w = n - which * D;
-          const int b = m / p.T, t = m - (m / p.T) * p.T;
-          const size_t bh = (size_t)b * p.heads + (w >> 6);
-          const float sc = (which == 0 && !F16) ? p.qscale : 1.f;
-          f16x8 h;
+          const int bh = qb * p.heads + (w >> 6);
+          f16x8 h = raw;
+          if constexpr (!RAW) {
+            const float sc = which == 0 ? p.qscale : 1.f;
 #pragma unroll
-          for (int r = 0; r < 8; ++r) h[r] = (f16)(v[r] * sc);
+            for (int r = 0; r < 8; ++r) h[r] = (f16)(v[r] * sc);
+          }
+          // 32-bit element offset: q / k hold B * heads * Tpad * 64 < 2^31 halves
           f16* dst = (which == 0 ? reinterpret_cast<f16*>(p.q) : reinterpret_cast<f16*>(p.k)) +
-                     (bh * p.Tpad + t) * 64 + (w & 63);
+                     (unsigned)((bh * p.Tpad + qt) * 64 + (w & 63));
           *reinterpret_cast<f16x8*>(dst) = h;
         }
       }

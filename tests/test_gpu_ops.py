@@ -383,7 +383,9 @@ def ln_partials_ref(xh):
     return torch.stack([v.sum(-1), m2], -1).transpose(0, 1).contiguous()
 
 
-@pytest.mark.parametrize("m,n,k", [(300, 384, 384), (38360, 384, 384), (1370, 384, 1536), (2740, 1024, 1024)])
+@pytest.mark.parametrize("m,n,k", [(300, 384, 384), (38360, 384, 384), (1370, 384, 1536), (2740, 1024, 1024),
+                                   # >= 512 tiles of 256 x 128: the 8-wave residual tile (gemm.hip dispatch)
+                                   (43840, 384, 384), (43850, 384, 1536)])
 def test_linear_residual_f16(gpu, m, n, k):
     """proj / fc2 over the f16 residual stream of precision "fp16" engines:
     xh += ls * (a W^T + b), fp32 update, one rounding to f16; plus the

@@ -47,6 +47,13 @@ VARIANTS = {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }""", """MDE_DEV void wait_vm_n() {
 }""", 1)]),
+    # candidate (not an ablation): static priority for the second-dispatched
+    # half of an 8-wave workgroup (MI355X_MICROARCH.md "Two waves per SIMD" 4)
+    "attn_prio": ("attention.hip", [
+        ("""  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  // XCD-aware block order""", """  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  // XCD-aware block order""", 1)]),
     # GEMM main loop only: the epilogue returns unless a NaN appears (r02's
     # MDE_EXP_NOEPI, profiles/r02_v10_epilogue_cost_*)
     "gemm_noepi": ("gemm.hip", [
