@@ -483,7 +483,10 @@ __global__ void splitk_store_kernel(const float* __restrict__ P, int S, int M, i
     for (int r = 0; r < 8; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
   } else if (p.act == ACT_GELU) {
 #pragma unroll
-    for (int r = 0; r < 8; ++r) v[r] = gelu_erf(v[r]);
+    for (int r = 0; r < 8; r += 2) {
+      const f32x2 g = gelu_erf2(f32x2{v[r], v[r + 1]});
+      v[r] = g[0], v[r + 1] = g[1];
+    }
   }
   const size_t o = (size_t)m * p.ldo + n;
   if (p.res0) {

@@ -37,6 +37,22 @@ MDE_DEV float gelu_erf(float x) {
   return x * __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(z));
 }
 
+// gelu_erf on two lanes' values at once: the polynomial on packed f32
+// (v_pk_mul_f32 / v_pk_fma_f32: 5 instructions for both elements), the
+// clamp, exp2 and reciprocal per element -- 11 VALU per pair instead of 18,
+// bit-identical to gelu_erf (same fused operations in the same order)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+MDE_DEV f32x2 gelu_erf2(f32x2 x) {
+  const f32x2 xc = {__builtin_amdgcn_fmed3f(x[0], -8.f, 8.f), __builtin_amdgcn_fmed3f(x[1], -8.f, 8.f)};
+  const f32x2 x2 = xc * xc;
+  const f32x2 c = {0.001014263055f, 0.001014263055f}, b = {-0.106775724f, -0.106775724f},
+              a = {-2.301121339f, -2.301121339f};
+  const f32x2 z = xc * __builtin_elementwise_fma(__builtin_elementwise_fma(c, x2, b), x2, a);
+  const f32x2 d = {1.f + __builtin_amdgcn_exp2f(z[0]), 1.f + __builtin_amdgcn_exp2f(z[1])};
+  const f32x2 r = {__builtin_amdgcn_rcpf(d[0]), __builtin_amdgcn_rcpf(d[1])};
+  return x * r;
+}
+
 // PyTorch upsample_bilinear2d(align_corners=True) source index and weights
 // (area_pixel_compute_scale / _source_index in fp32, then floor, clamp of the
 // +1 neighbour, lambda = src - i0), each op rounded as on the CPU: contraction

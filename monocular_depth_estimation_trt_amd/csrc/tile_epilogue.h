@@ -86,8 +86,8 @@ MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&m
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
           } else if (p.act == ACT_GELU) {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
+            const f32x2 lo = gelu_erf2(f32x2{v[0], v[1]}), hi = gelu_erf2(f32x2{v[2], v[3]});
+            v[0] = lo[0], v[1] = lo[1], v[2] = hi[0], v[3] = hi[1];
           }
           const size_t o = (size_t)m * p.ldo + n;
           if (p.res0) {
@@ -257,9 +257,13 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
     }
 
     // ---- phase 1: accumulator rows [PS*R/NP, (PS+1)*R/NP) (+bias, activation) -> LDS ----
-    auto park = [&](auto ps_tag, auto np_tag, auto f16_tag) {
+    // (the activation is a template tag: one uniform branch per tile, not
+    // per fragment -- a runtime switch inside the unrolled loop costs every
+    // fragment its moves, branches and re-materialised constants)
+    auto park_act = [&](auto ps_tag, auto np_tag, auto f16_tag, auto act_tag) {
       constexpr int PS = decltype(ps_tag)::value, NP = decltype(np_tag)::value;
       constexpr bool F16 = decltype(f16_tag)::value;
+      constexpr int ACT = decltype(act_tag)::value;
       const float sc = (EM == E_QKV && F16 && which == 0) ? p.qscale : 1.f;  // f16 rows carry the q scale
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -268,14 +272,12 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
         for (int i = PS * (TM / NP); i < (PS + 1) * (TM / NP); ++i) {
           f32x4 v = acc[i][j];
           v[0] += bn.x; v[1] += bn.y; v[2] += bn.z; v[3] += bn.w;
-          if constexpr (EM == E_STORE) {
-            if (p.act == ACT_RELU) {
+          if constexpr (ACT == ACT_RELU) {
 #pragma unroll
-              for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
-            } else if (p.act == ACT_GELU) {
-#pragma unroll
-              for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
-            }
+            for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+          } else if constexpr (ACT == ACT_GELU) {
+            const f32x2 lo = gelu_erf2(f32x2{v[0], v[1]}), hi = gelu_erf2(f32x2{v[2], v[3]});
+            v = f32x4{lo[0], lo[1], hi[0], hi[1]};
           }
           const int row = (i - PS * (TM / NP)) * 16 + (lane & 15);
           if constexpr (F16) {
@@ -288,6 +290,13 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
       }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_wave_barrier();
+    };
+    auto park = [&](auto ps_tag, auto np_tag, auto f16_tag) {
+      if constexpr (EM == E_STORE) {
+        if (p.act == ACT_GELU) return park_act(ps_tag, np_tag, f16_tag, std::integral_constant<int, ACT_GELU>{});
+        if (p.act == ACT_RELU) return park_act(ps_tag, np_tag, f16_tag, std::integral_constant<int, ACT_RELU>{});
+      }
+      park_act(ps_tag, np_tag, f16_tag, std::integral_constant<int, ACT_NONE>{});
     };
     // 4 staged values of row `row`, 16-B fp32 chunk / 8-B f16 quad `ch`
     auto rd4 = [&](auto f16_tag, int row, int ch) -> f32x4 {

@@ -1,6 +1,7 @@
 """Build ablation variants of libmde_hip.so without touching the product source.
 
     python tools/ablate.py NAME            -> build/var/lib_NAME.so
+    python tools/ablate.py --rev HEAD      -> build/var/lib_rev_HEAD.so (A/B side)
 
 Each variant copies csrc/ to build/ablate/NAME/, applies text substitutions
 to one kernel file (asserting each pattern is present) and links a library
@@ -108,6 +109,49 @@ def build(name: str) -> str:
     return out
 
 
+def build_rev(rev: str) -> str:
+    """The whole library as of git revision `rev` (the A side of an A/B
+    against the working tree): build/var/lib_rev_<rev>.so"""
+    import concurrent.futures as cf
+    import tarfile
+    import io
+    from monocular_depth_estimation_trt_amd import _build
+    sha = subprocess.run(["git", "rev-parse", "--short", rev], cwd=ROOT, capture_output=True, text=True,
+                         check=True).stdout.strip()
+    work = os.path.join(ROOT, "build", "ablate", f"rev_{sha}")
+    if os.path.exists(work):
+        shutil.rmtree(work)
+    os.makedirs(work)
+    tar = subprocess.run(["git", "archive", sha, "monocular_depth_estimation_trt_amd/csrc", "include"], cwd=ROOT,
+                         capture_output=True, check=True).stdout
+    with tarfile.open(fileobj=io.BytesIO(tar)) as t:
+        t.extractall(work)
+    csrc = os.path.join(work, "monocular_depth_estimation_trt_amd", "csrc")
+    inc = os.path.join(work, "include")
+    flags = [f if f not in (_build.CSRC, _build.INCLUDE) else (csrc if f == _build.CSRC else inc) for f in _build.FLAGS]
+    cc = _build.hipcc()
+
+    def one(src):
+        obj = os.path.join(work, src + ".o")
+        r = subprocess.run([cc, *flags, *_build.PER_FILE.get(src, []), "-c", os.path.join(csrc, src), "-o", obj],
+                           capture_output=True, text=True)
+        if r.returncode:
+            raise SystemExit(f"rev {sha}: hipcc failed on {src}\n{r.stderr[-3000:]}")
+        return obj
+
+    with cf.ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 4)) as ex:
+        objs = list(ex.map(one, _build.SOURCES))
+    out = os.path.join(ROOT, "build", "var", f"lib_rev_{rev}.so")
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    subprocess.run([cc, f"--offload-arch={_build.ARCH}", "-shared", "-fPIC", "-o", out, *objs], check=True)
+    print(f"[ablate] built {out} ({sha})")
+    return out
+
+
 if __name__ == "__main__":
-    for n in sys.argv[1:] or sorted(VARIANTS):
-        build(n)
+    args = sys.argv[1:]
+    if args[:1] == ["--rev"]:
+        build_rev(args[1] if len(args) > 1 else "HEAD")
+    else:
+        for n in args or sorted(VARIANTS):
+            build(n)
