@@ -14,6 +14,8 @@
 // through a double-buffered LDS stage per tap.  Patch rows are CK*2 bytes
 // with the chunk swizzle of the GEMM (c ^ (pix & 7) for 128-B rows,
 // c ^ ((pix >> 1) & 3) for 64-B rows): conflict-free fragment reads at S = 1.
+#include <cstdlib>
+
 #include "mde_device.h"
 #include "mde_ops.h"
 #include "tile_epilogue.h"
@@ -346,6 +348,357 @@ hipError_t conv_tiles(const GemmParams& p, hipStream_t st) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Separable upsampling conv (A_CONV3_UP, 32 output channels: the DPT head's
+// output_conv1 at ViT-S and output_conv2 at every width).
+//
+// conv3_kernel's upsampling loader blends each virtual pixel of its 10 x 18
+// patch from 4 source taps: 4 loads and 3 lerps per pixel, 1.4 virtual
+// pixels per output, and every 128-pixel workgroup restages the 9 weight
+// taps.  The bilinear upsample is separable, so this kernel builds the patch
+// in two passes over a 16 x 16 output tile (18 x 18 virtual patch):
+//   pass H: for each source row the tile touches (<= 13) and each patch
+//           column, lerp the two source columns (2 loads, 1 lerp);
+//   pass V: for each patch pixel, lerp the two H rows (2 LDS reads, 1 lerp).
+// Per output pixel: ~1.7 loads and ~2.1 lerps instead of 5.6 and 4.2, and
+// the weights (all 9 taps x cc, <= 72 KB) are staged once per 256 pixels.
+// The blend is the same two-level lerp in the same order (horizontal, then
+// vertical) as conv3_kernel, so the patch is bit-identical; at cc = 32 the
+// MFMA order is too (cc > 32: 32-channel chunks, tap-major inside a chunk).
+// 8 waves x (2 tile rows x 32 channels); LDS (cc = 32) 53 KB: three
+// workgroups per CU.
+constexpr int UTH = 16, UTW = 16;                        // output tile
+constexpr int UPH = UTH + 2, UPW = UTW + 2;              // virtual patch
+constexpr int USR = 13;                                  // source rows per tile (host-checked)
+constexpr int UPATCH = UPH * UPW * 64, UHBUF = USR * UPW * 64;
+
+template <int NCH, int EM, bool PERSIST>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NCH == 1 ? 6 : 4)))
+upconv_kernel(const GemmParams p) {
+  static_assert(EM == E_STORE || EM == E_HEAD, "upconv epilogues");
+  constexpr int NT = 512, TM = 2, TN = 2;
+  constexpr int WROWS = 9 * NCH * 32;  // weight rows of 64 B: (tap, chunk, out channel)
+  // E_STORE stages f16 rows (store_tile_lds HALF: 2 KB per wave) in the patch
+  // space, which no wave writes again before the next item's first barrier
+  // bias (and the head's 1x1 weights) live in LDS: a global load in the
+  // epilogue would wait (vmcnt is in order) for the next item's prefetch
+  __shared__ __attribute__((aligned(16))) char smem[UPATCH + UHBUF + WROWS * 64 + 256];
+  char* const sP = smem;
+  char* const sH = smem + UPATCH;
+  char* const sW = sH + UHBUF;
+  float* const sBias = reinterpret_cast<float*>(sW + WROWS * 64);  // [32] bias, [32] w2 (E_HEAD)
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Ho = p.oh, Wo = p.ow;
+  const int tiles_x = (Wo + UTW - 1) / UTW, tiles_y = (Ho + UTH - 1) / UTH;
+  const int ntiles = p.cb * tiles_x * tiles_y;
+  // tiles of this workgroup: t, t + tstep, ... < tend.  Persistent: XCD x
+  // (= blockIdx % 8, one L2) owns the contiguous range [x nt / 8, (x+1) nt / 8)
+  // and its workgroups stride through it, so the tiles an XCD has in flight
+  // are neighbours sharing their source rows in its L2.
+  int t, tstep, tend;
+  if constexpr (PERSIST) {
+    const int x = blockIdx.x & 7, g8 = (int)gridDim.x >> 3;
+    t = (int)((long long)x * ntiles / 8) + (int)(blockIdx.x >> 3);
+    tend = (int)((long long)(x + 1) * ntiles / 8);
+    tstep = g8;
+  } else {
+    t = xcd_remap(blockIdx.x, gridDim.x);
+    tend = t + 1;
+    tstep = 1;
+  }
+  if (t >= tend) return;  // uniform, before any load is issued
+  const float usy = ac_scale(p.ch, p.uh), usx = ac_scale(p.cw, p.uw);
+  const unsigned rowstride = (unsigned)p.cw * (unsigned)p.cc;
+
+  // ---- weights, all taps and chunks, once (glds: 16 rows x 4 chunks per wave-instruction)
+  {
+    const int lrow = lane >> 2, lch = cpch<32>(lrow, lane & 3);
+    for (int q = wave; q < WROWS / 16; q += 8) {
+      const int tc = q >> 1, n = (q & 1) * 16 + lrow;
+      const int tp = tc / NCH, c = tc - (tc / NCH) * NCH;
+      glds16c(reinterpret_cast<const f16*>(p.W) + (size_t)n * p.ldw + tp * p.cc + c * 32 + lch * 8, sW + q * 16 * 64);
+    }
+  }
+
+  if (tid < 64) {
+    const float* src = tid < 32 ? p.bias : p.w2;
+    sBias[tid] = (src && (tid < 32 || EM == E_HEAD)) ? src[tid & 31] : 0.f;
+  }
+
+  // tile geometry: image, tile row / column, virtual origin, source rows [sy0, sy0 + nsr)
+  struct Geo {
+    int b, ty, tx, iy0, ix0, sy0, nsr;
+  };
+  auto geo = [&](int tt) {
+    Geo g;
+    g.tx = tt % tiles_x;
+    const int r = tt / tiles_x;
+    g.ty = r % tiles_y;
+    g.b = r / tiles_y;
+    g.iy0 = g.ty * UTH - 1;
+    g.ix0 = g.tx * UTW - 1;
+    int a0, a1, b0, b1;
+    float l0, l1;
+    ac_index(usy, g.iy0 < 0 ? 0 : g.iy0, p.ch, a0, a1, l0, l1);
+    const int last = g.iy0 + UPH - 1 < p.uh - 1 ? g.iy0 + UPH - 1 : p.uh - 1;
+    ac_index(usy, last, p.ch, b0, b1, l0, l1);
+    g.sy0 = a0;
+    g.nsr = b1 - a0 + 1 < USR ? b1 - a0 + 1 : USR;
+    return g;
+  };
+
+  // ---- pass H operands of item (tile g, chunk c): HI (source row, patch
+  // column, 8-channel chunk) items per thread, both source columns loaded
+  // into registers -- issued one item ahead, under the previous item's
+  // pass V, MFMAs and epilogue
+  constexpr int HI = (USR * UPW * 4 + NT - 1) / NT;
+  f16x8 ha[HI], hb[HI];
+  f16 hw[HI];
+  bool hs[HI], hin[HI];
+  auto h_issue = [&](const Geo& g, int c, int tid) {
+    const f16* img = reinterpret_cast<const f16*>(p.A) + (size_t)g.b * p.ch * p.cw * p.cc;
+#pragma unroll
+    for (int k = 0; k < HI; ++k) {
+      const int it = tid + k * NT;
+      const int lc = it & 3, rest = it >> 2;
+      const int sr = rest / UPW, col = rest - (rest / UPW) * UPW;
+      const int ix = g.ix0 + col;
+      hs[k] = it < g.nsr * UPW * 4;
+      const bool in = hs[k] && ix >= 0 && ix < p.uw;
+      hin[k] = in;
+      int x0 = 0, x1 = 0;
+      float lx0, lx1 = 0.f;
+      if (in) ac_index(usx, ix, p.cw, x0, x1, lx0, lx1);
+      hw[k] = (f16)lx1;
+      const unsigned r = (unsigned)(g.sy0 + (in ? sr : 0)) * rowstride + (unsigned)(c * 32 + lc * 8);
+      // (out-of-map columns load a valid pixel and are zeroed at the commit:
+      // a select here would wait for the load)
+      ha[k] = *reinterpret_cast<const f16x8*>(img + (r + (unsigned)x0 * (unsigned)p.cc));
+      hb[k] = *reinterpret_cast<const f16x8*>(img + (r + (unsigned)x1 * (unsigned)p.cc));
+    }
+  };
+  auto h_commit = [&](int tid) {
+#pragma unroll
+    for (int k = 0; k < HI; ++k) {
+      const int it = tid + k * NT;
+      if (hs[k]) {
+        const int lc = it & 3, hp = it >> 2;  // hp = sr * UPW + col
+        *reinterpret_cast<f16x8*>(sH + hp * 64 + cpch<32>(hp, lc) * 16) =
+            hin[k] ? lerp8(ha[k], hb[k], hw[k]) : zero8();
+      }
+    }
+  };
+
+  f32x4 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Geo g = geo(t);
+  int c = 0;
+  h_issue(g, 0, tid);
+  for (;;) {
+    // the thread id through an opaque move: every lane-derived LDS address is
+    // recomputed per item instead of being hoisted out of the tile loop (the
+    // 18 tap addresses of the patch fragments alone would hold 18 VGPRs)
+    int vt;
+    asm volatile("v_mov_b32 %0, %1" : "=v"(vt) : "v"(tid));
+    const int vl = vt & 63;
+    wait_vmc();  // this item's pass-H operands (and, first time, the weights) landed
+    h_commit(vt);
+    __syncthreads();  // H complete; every wave done with the previous item's MFMAs / staging
+    // the next item's pass-H loads fly under this item's pass V, MFMAs and epilogue
+    int tn = t, cn = c + 1;
+    if (cn == NCH) {
+      cn = 0;
+      tn = t + tstep;
+    }
+    Geo gn = g;
+    if (tn < tend) {
+      gn = geo(tn);
+      h_issue(gn, cn, vt);
+    }
+    // ---- pass V: (patch pixel, chunk) items (not unrolled: the next item's
+    // pass-H registers are live here)
+#pragma unroll 1
+    for (int it = vt; it < UPH * UPW * 4; it += NT) {
+      const int lc = it & 3, pp = it >> 2;
+      const int r = pp / UPW, col = pp - (pp / UPW) * UPW;
+      const int iy = g.iy0 + r, ix = g.ix0 + col;
+      f16x8 v = zero8();
+      if (iy >= 0 && iy < p.uh && ix >= 0 && ix < p.uw) {
+        int y0, y1;
+        float ly0, ly1;
+        ac_index(usy, iy, p.ch, y0, y1, ly0, ly1);
+        const int h0 = (y0 - g.sy0) * UPW + col, h1 = (y1 - g.sy0) * UPW + col;
+        const f16x8 a = *reinterpret_cast<const f16x8*>(sH + h0 * 64 + cpch<32>(h0, lc) * 16);
+        const f16x8 bb = *reinterpret_cast<const f16x8*>(sH + h1 * 64 + cpch<32>(h1, lc) * 16);
+        v = lerp8(a, bb, (f16)ly1);
+        if (p.relu_in) v = relu8(v);
+      }
+      *reinterpret_cast<f16x8*>(sP + pp * 64 + cpch<32>(pp, lc) * 16) = v;
+    }
+    __syncthreads();
+    // ---- 9 taps x one 32-deep k-step of chunk c
+    {
+      const int lane = vl, lc = vl >> 4;
+#pragma unroll
+      for (int tp = 0; tp < 9; ++tp) {
+        const int ky = tp / 3, kx = tp - (tp / 3) * 3;
+        f16x8 fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int pp = (wave * TM + i + ky) * UPW + (lane & 15) + kx;
+          fa[i] = *reinterpret_cast<const f16x8*>(sP + pp * 64 + cpch<32>(pp, lc) * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int r = j * 16 + (lane & 15);
+          fb[j] = *reinterpret_cast<const f16x8*>(sW + ((tp * NCH + c) * 32 + r) * 64 + cpch<32>(r, lc) * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);
+        if constexpr (PERSIST) __builtin_amdgcn_sched_barrier(0);  // no fragment hoisting across taps (registers)
+      }
+    }
+    if (c == NCH - 1) {
+      // ---- epilogue of tile t: lane owns pixel (row wave*TM + i, column
+      // lane & 15) and channels 16 j + 4 (lane >> 4) + r (tile_epilogue.h
+      // store_tile semantics, bias from LDS)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int oy = g.ty * UTH + wave * TM + i, ox = g.tx * UTW + (vl & 15);
+        const int m = (oy < Ho && ox < Wo) ? ((g.b * Ho + oy) * Wo + ox) : -1;
+        if constexpr (EM == E_HEAD) {
+          // (the positional-embedding variant in its own branch: its global
+          // load's wait must not sit on the no-pe path, where it would drain
+          // the next item's prefetch)
+          auto hidden = [&](auto pe_tag) {
+            constexpr bool PE = decltype(pe_tag)::value;
+            float part = 0.f;
+#pragma unroll
+            for (int j = 0; j < TN; ++j) {
+              const int n0 = j * 16 + (vl >> 4) * 4;
+              const float4 bn = *reinterpret_cast<const float4*>(sBias + n0);
+              const float4 w2 = *reinterpret_cast<const float4*>(sBias + 32 + n0);
+              float pv[4] = {0.f, 0.f, 0.f, 0.f};
+              if constexpr (PE) {
+                if (m >= 0) {
+                  const f16x4 q = *reinterpret_cast<const f16x4*>(reinterpret_cast<const f16*>(p.hpe) +
+                                                                  (size_t)(m % p.hpe_pix) * 32 + n0);
+#pragma unroll
+                  for (int r = 0; r < 4; ++r) pv[r] = (float)q[r];
+                }
+              }
+              const float h0 = acc[i][j][0] + bn.x + pv[0], h1 = acc[i][j][1] + bn.y + pv[1];
+              const float h2 = acc[i][j][2] + bn.z + pv[2], h3 = acc[i][j][3] + bn.w + pv[3];
+              // explicit fma chain: the contraction store_tile's loop gets
+              // (packed-math vectorisation would otherwise split some of it)
+              part = fmaf(h0 > 0.f ? h0 : 0.f, w2.x, part);
+              part = fmaf(h1 > 0.f ? h1 : 0.f, w2.y, part);
+              part = fmaf(h2 > 0.f ? h2 : 0.f, w2.z, part);
+              part = fmaf(h3 > 0.f ? h3 : 0.f, w2.w, part);
+            }
+            return part;
+          };
+          float part = p.hpe ? hidden(std::true_type{}) : hidden(std::false_type{});
+          part += __shfl_xor(part, 16, 64);
+          part += __shfl_xor(part, 32, 64);
+          if ((vl >> 4) == 0 && m >= 0) {
+            const float z = part + p.b2;
+            p.out32[m] = p.head_metric == 2 ? __expf(z)
+                         : p.head_metric ? p.max_depth / (1.f + __expf(-z)) : (z > 0.f ? z : 0.f);
+          }
+        } else {
+          if (m < 0) continue;
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            const int n0 = j * 16 + (vl >> 4) * 4;
+            const float4 bn = *reinterpret_cast<const float4*>(sBias + n0);
+            float v[4] = {acc[i][j][0] + bn.x, acc[i][j][1] + bn.y, acc[i][j][2] + bn.z, acc[i][j][3] + bn.w};
+            if (p.act == ACT_RELU) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
+            } else if (p.act == ACT_GELU) {
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] = gelu_erf(v[r]);
+            }
+            const f16x4 h = {(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
+            *reinterpret_cast<f16x4*>(reinterpret_cast<f16*>(p.out16) + (size_t)m * p.ldo + n0) = h;
+          }
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    if (tn >= tend) break;
+    t = tn;
+    c = cn;
+    g = gn;
+  }
+}
+
+// MDE_UPCONV=0: the upsampling convs stay on conv3_kernel (A/B; read per
+// call so a test can compare both kernels -- captured graphs keep their choice)
+bool upconv_enabled() {
+  const char* e = getenv("MDE_UPCONV");
+  return !(e && e[0] == '0');
+}
+
+// a 16-row tile's 18 virtual rows must come from at most USR source rows:
+// (UPH - 1) * scale + 2 rows, with a one-row margin for the float index
+bool upconv_eligible(const GemmParams& p) {
+  if (p.amode != A_CONV3_UP || p.N != 32 || p.stride != 1 || (p.cc & 31) || p.cc > 128) return false;
+  if (p.emode != E_STORE && p.emode != E_HEAD) return false;
+  if (p.emode == E_STORE && ((p.ldo & 3) || p.res0 || p.res1)) return false;
+  if (p.uh < 2 || p.uw < 1 || p.ch < 1 || p.cw < 1) return false;
+  const double sy = (double)(p.ch - 1) / (double)(p.uh - 1);
+  return sy * (UPH - 1) + 3.0 <= (double)USR && upconv_enabled();
+}
+
+// persistent grid: workgroups per CU the LDS allows x 256 CUs (MDE_UPCONV_PERSIST=0: one tile per workgroup)
+template <int NCH>
+int upconv_grid() {
+  constexpr int lds = UPATCH + UHBUF + 9 * NCH * 32 * 64;
+  const int per_cu = 163840 / lds < 4 ? 163840 / lds : 4;
+  return 256 * (per_cu > 0 ? per_cu : 1);
+}
+bool upconv_persist() {
+  const char* e = getenv("MDE_UPCONV_PERSIST");
+  return !(e && e[0] == '0');
+}
+
+template <int NCH, int EM>
+void launch_upconv_n(const GemmParams& p, long long tiles, hipStream_t st) {
+  const int grid = upconv_grid<NCH>();
+  if (upconv_persist() && tiles > grid)
+    hipLaunchKernelGGL((upconv_kernel<NCH, EM, true>), dim3((unsigned)grid), dim3(512), 0, st, p);
+  else
+    hipLaunchKernelGGL((upconv_kernel<NCH, EM, false>), dim3((unsigned)tiles), dim3(512), 0, st, p);
+}
+
+template <int EM>
+hipError_t launch_upconv(const GemmParams& p, hipStream_t st) {
+  const long long tiles = (long long)p.cb * ((p.oh + UTH - 1) / UTH) * ((p.ow + UTW - 1) / UTW);
+  if (tiles <= 0) return hipSuccess;
+  if (tiles >= (1ll << 31)) return hipErrorInvalidValue;
+  switch (p.cc / 32) {
+    case 1: launch_upconv_n<1, EM>(p, tiles, st); break;
+    case 2: launch_upconv_n<2, EM>(p, tiles, st); break;
+    case 3: launch_upconv_n<3, EM>(p, tiles, st); break;
+    case 4: launch_upconv_n<4, EM>(p, tiles, st); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 }  // namespace
 
 bool conv_direct_supported(const GemmParams& p) {
@@ -358,6 +711,7 @@ hipError_t launch_conv3(const GemmParams& p, hipStream_t st) {
   if (p.M <= 0 || p.N <= 0) return hipSuccess;
   if (!conv_direct_supported(p) || (p.N & 7) || (p.ldw & 63) || p.ldw < 9 * p.cc) return hipErrorInvalidValue;
   const bool up = p.amode == A_CONV3_UP;
+  if (up && upconv_eligible(p)) return p.emode == E_HEAD ? launch_upconv<E_HEAD>(p, st) : launch_upconv<E_STORE>(p, st);
   const bool ck64 = (p.cc % 64) == 0 && p.stride == 1;
   if (p.emode == E_HEAD) {
     if (p.N != 32 || p.stride != 1) return hipErrorInvalidValue;

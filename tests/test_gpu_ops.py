@@ -296,7 +296,10 @@ def test_linear_splitk(gpu, m, n, k, act):
 
 
 @pytest.mark.parametrize("B,sh,sw,uh,uw,cin,cout", [(1, 10, 10, 19, 19, 64, 32), (2, 16, 12, 28, 21, 32, 64),
-                                                    (1, 148, 148, 296, 296, 64, 32), (2, 40, 40, 73, 71, 32, 32)])
+                                                    (1, 148, 148, 296, 296, 64, 32), (2, 40, 40, 73, 71, 32, 32),
+                                                    # separable upconv kernel: 96 / 128 channels, 1-pixel-wide map
+                                                    (2, 37, 45, 64, 77, 128, 32), (1, 18, 3, 33, 5, 96, 32),
+                                                    (1, 74, 74, 130, 130, 32, 32)])
 def test_conv3x3_up(gpu, B, sh, sw, uh, uw, cin, cout):
     x = rn(B, cin, sh, sw)
     wt, b = rn(cout, cin, 3, 3, scale=(9 * cin) ** -0.5), rn(cout, scale=0.02)
@@ -363,6 +366,45 @@ def test_depth_head(gpu, metric):
     op("mde_op_depth_head", ptr(nhwc(x).half().to(gpu)), B, sh, sw, cin, uh, uw, ptr(wp), wp.shape[1],
        ptr(b1.to(gpu)), ptr(w2.to(gpu)), b2, metric, 20.0, ptr(out), stream())
     close(out, ref, 1e-2, 2e-2, "depth_head")
+
+
+@pytest.mark.parametrize("B,sh,sw,uh,uw,cin,head", [(2, 296, 296, 518, 518, 32, 1), (1, 148, 148, 296, 296, 64, 0),
+                                                   (3, 21, 17, 37, 30, 32, 1), (2, 37, 45, 64, 77, 128, 0),
+                                                   (1, 9, 40, 16, 70, 32, 0), (1, 1, 1, 1, 1, 32, 1),
+                                                   # grids past the persistent size at 64 / 128 channels
+                                                   (2, 148, 148, 296, 296, 64, 0), (2, 100, 100, 200, 200, 128, 1)])
+def test_upconv_matches_conv3(gpu, monkeypatch, B, sh, sw, uh, uw, cin, head):
+    """The separable upsampling conv (conv.hip upconv_kernel, persistent when
+    the grid exceeds what the chip holds at once) against the 4-tap
+    conv3_kernel it replaces (MDE_UPCONV=0): the same two-level f16
+    blend in the same order, so at 32 input channels (one chunk, same MFMA
+    order) the outputs are bit-identical; wider inputs sum 32-channel chunks
+    in another order (fp32), within one f16 ulp."""
+    x = rn(B, cin, sh, sw)
+    w1, b1 = rn(32, cin, 3, 3, scale=(9 * cin) ** -0.5), rn(32, scale=0.02)
+    w2 = rn(32, scale=32 ** -0.5)
+    wp = conv_w(w1).to(gpu)
+    xin = nhwc(x).half().to(gpu)
+    outs = []
+    for flag, persist in (("0", "1"), ("1", "1"), ("1", "0")):  # conv3_kernel, persistent upconv, one tile per workgroup
+        monkeypatch.setenv("MDE_UPCONV", flag)
+        monkeypatch.setenv("MDE_UPCONV_PERSIST", persist)
+        if head:
+            out = torch.empty(B, uh, uw, device=gpu)
+            op("mde_op_depth_head", ptr(xin), B, sh, sw, cin, uh, uw, ptr(wp), wp.shape[1], ptr(b1.to(gpu)),
+               ptr(w2.to(gpu)), 0.05, 1, 20.0, ptr(out), stream())
+        else:
+            out = torch.empty(B, uh, uw, 32, dtype=torch.float16, device=gpu)
+            op("mde_op_conv3x3_up", ptr(xin), B, sh, sw, cin, uh, uw, ptr(wp), wp.shape[1], 32, ptr(b1.to(gpu)), 0,
+               ptr(out), stream())
+        torch.cuda.synchronize()
+        outs.append(out.float().cpu())
+    old, new, single = outs
+    assert torch.equal(new, single), (new - single).abs().max()
+    if cin == 32:
+        assert torch.equal(old, new), (old - new).abs().max()
+    else:
+        assert torch.allclose(old, new, rtol=2e-3, atol=2e-3), (old - new).abs().max()
 
 
 def test_bad_arguments_raise(gpu):

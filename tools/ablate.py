@@ -72,6 +72,23 @@ VARIANTS = {
     "gemm_nomfma": ("gemm.hip", [
         ("for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);",
          'for (int j = 0; j < TN; ++j) asm volatile("" :: "v"(fb[j]), "v"(fa[i]));', 1)]),
+    # direct conv, upsampling patch: one source tap per virtual pixel, no blend
+    "conv_noblend": ("conv.hip", [
+        ("""            const f16x8 bq = *reinterpret_cast<const f16x8*>(img + (r0 + o1 + lc * 8));
+            const f16x8 c = *reinterpret_cast<const f16x8*>(img + (r1 + o0 + lc * 8));
+            const f16x8 d = *reinterpret_cast<const f16x8*>(img + (r1 + o1 + lc * 8));""", "", 1),
+        ("v = lerp8(lerp8(a, bq, (f16)lx1), lerp8(c, d, (f16)lx1), (f16)ly1);", "v = a;", 1)]),
+    # direct conv: no MFMAs (fragments kept live)
+    "conv_nomfma": ("conv.hip", [
+        ("for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);",
+         'for (int j = 0; j < TN; ++j) asm volatile("" :: "v"(fb[j]), "v"(fa[i]));', 2)]),
+    # direct conv: weights never loaded (LDS garbage)
+    "conv_now": ("conv.hip", [
+        ("for (int q = wave; q < BINS; q += NW) glds16c(", "for (int q = wave; q < 0; q += NW) glds16c(", 1)]),
+    # direct conv: no patch at all (LDS garbage): weights, MFMA and epilogue only
+    "conv_nopatch": ("conv.hip", [
+        ("  auto load_patch = [&](int chunk) {\n    const int cbase = chunk * CK;",
+         "  auto load_patch = [&](int chunk) {\n    if (chunk >= 0) return;\n    const int cbase = chunk * CK;", 1)]),
 }
 
 
