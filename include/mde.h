@@ -180,6 +180,13 @@ int mde_op_attention(const void* q_f16, const void* k_f16, const void* vt_f16, v
 int mde_op_attention_ws(const void* q_f16, const void* k_f16, const void* vt_f16, void* o_f16, int batch, int heads,
                         int tokens, int tokens_pad, int ldo, void* ws, size_t ws_bytes, void* stream);
 size_t mde_op_attention_ws_bytes(int batch, int heads, int tokens);
+/* mde_op_attention_ws with an explicit launch configuration (tests / tuning; no reference
+ * counterpart): cfg = "<waves>[s<split>][g<groups>]", e.g. "8" (256-query workgroups), "4s2"
+ * (split-KV over two workgroups + merge kernel, needs ws), "4g2" (two key groups of 64 queries
+ * inside one workgroup, merged through LDS); NULL or "" = the launcher's policy. */
+int mde_op_attention_cfg(const void* q_f16, const void* k_f16, const void* vt_f16, void* o_f16, int batch, int heads,
+                         int tokens, int tokens_pad, int ldo, const char* cfg, void* ws, size_t ws_bytes,
+                         void* stream);
 int mde_op_patch_embed(const float* img, int batch, int h, int w, const void* w_f16, int ldw, const float* bias,
                        const float* pos_patch, const float* cls_pos, int dim, void* patch_scratch_f16,
                        float* x32, void* stream);

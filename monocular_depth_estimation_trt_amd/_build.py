@@ -45,7 +45,9 @@ def _digest() -> str:
             h.update(f.read())
     with open(os.path.join(INCLUDE, "mde.h"), "rb") as f:
         h.update(f.read())
-    h.update(" ".join(FLAGS).encode())
+    # flags without the checkout's absolute paths: the same tree at another
+    # path (the GPU box's copy) is the same build
+    h.update(" ".join(FLAGS).replace(ROOT, "<root>").encode())
     h.update(repr(sorted(PER_FILE.items())).encode())
     return h.hexdigest()
 

@@ -97,6 +97,8 @@ PROTOTYPES = {
     "mde_op_attention_ws": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                             c_size_t, c_void_p],
     "mde_op_attention_ws_bytes": [c_int, c_int, c_int],
+    "mde_op_attention_cfg": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_char_p,
+                             c_void_p, c_size_t, c_void_p],
     "mde_op_attention": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "mde_op_patch_embed": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                            c_void_p, c_void_p, c_void_p],

@@ -121,23 +121,38 @@ struct SplitWs {
   int tiles = 0;        // key tiles per split
 };
 
-template <int NW, bool SPLIT, int R, int QS = 1>
+// Per-lane bytes one wave of a key group > 0 parks for the in-workgroup merge:
+// O^T (32 fp32) + (m, l)
+constexpr int MERGE_WAVE_B = 64 * 34 * 4;
+
+template <int NW, bool SPLIT, int R, int QS = 1, int NS = 1>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(QS == 2 ? 2 : 4, 8)))
 attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16* __restrict__ vt,
                 f16* __restrict__ o, int H, int T, int Tpad, int ldo, SplitWs ws) {
   // QS = 2: each wave owns two 32-query sub-tiles; every K / V^T fragment
-  // read feeds both, and one sub-tile's softmax overlaps the other's MFMAs
-  static_assert(QS == 1 || (QS == 2 && !SPLIT), "query sub-tiles per wave");
-  constexpr int BQ = QW * NW * QS;  // queries per workgroup
-  constexpr int INS = 8 / NW;    // glds instructions per wave per image (8 per 64-row image)
+  // read feeds both, and one sub-tile's softmax overlaps the other's MFMAs.
+  // NS > 1 (small grids): the workgroup's waves form NS key GROUPS of NW / NS
+  // query waves; group g walks the g-th slice of the key tiles for the same
+  // queries, each with its own K / V^T ring slots, and the groups' (O, m, l)
+  // merge through LDS after the loop -- the split-KV parallelism without the
+  // fp32 workspace round trip or a second kernel.
+  static_assert(QS == 1 || (QS == 2 && !SPLIT && NS == 1), "query sub-tiles per wave");
+  static_assert(NS == 1 || (!SPLIT && R == 2), "key groups");
+  constexpr int NWQ = NW / NS;       // query waves per key group
+  constexpr int BQ = QW * NWQ * QS;  // queries per workgroup
+  constexpr int INS = 8 / NWQ;       // glds instructions per wave per image (8 per 64-row image)
   constexpr int PER_TILE = 2 * INS;  // vmcnt entries one tile adds per wave (K + V^T)
+  static_assert(NWQ * NS == NW && (NWQ == 1 || NWQ == 2 || NWQ == 4 || NWQ == 8), "waves per key group");
   static_assert(NW == 4 || NW == 8, "waves per workgroup");
   static_assert(R >= 2 && R <= 4, "ring depth");
   constexpr int DIST = R - 1;  // tiles in flight ahead of the one computed
-  __shared__ __attribute__((aligned(16))) char smem[R * SLOT];
+  constexpr int RING_B = R * NS * SLOT, MERGE_B = (NS - 1) * NWQ * MERGE_WAVE_B;
+  __shared__ __attribute__((aligned(16))) char smem[RING_B > MERGE_B ? RING_B : MERGE_B];
 
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = NS > 1 ? wave_all / NWQ : 0;   // key group
+  const int wave = wave_all - grp * NWQ;         // query wave within the group
   // XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs
   // (linear id % 8 shares an L2); remap so each XCD takes a contiguous run
   // of (head, query block) pairs and a head's K/V^T is fetched into one L2,
@@ -151,10 +166,13 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
   const bool active = qbase < T;  // wave-uniform: a wave past the last query only helps load
   const int l31 = lane & 31, hh = lane >> 5;
 
-  // key tiles [kt0, kt1) of this workgroup (all of them unless split)
+  // key tiles [kt0, kt1) of this workgroup / key group (all of them unless
+  // split); every group steps ktl - kt0 times (uniform barrier count)
   const int nkt_all = (T + KT - 1) / KT;
-  const int kt0 = SPLIT ? (int)blockIdx.z * ws.tiles : 0;
-  const int kt1 = SPLIT ? min(nkt_all, kt0 + ws.tiles) : nkt_all;
+  const int gper = (nkt_all + NS - 1) / NS;  // tiles per key group
+  const int kt0 = SPLIT ? (int)blockIdx.z * ws.tiles : grp * gper;
+  const int kt1 = SPLIT ? min(nkt_all, kt0 + ws.tiles) : min(nkt_all, kt0 + gper);
+  const int ktl = NS > 1 ? kt0 + gper : kt1;
 
   const f16* qb = q + (size_t)bh * Tpad * 64;
   const f16* kb = k + (size_t)bh * Tpad * 64;
@@ -173,8 +191,9 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
 
   // glds geometry: lane -> row lrow of an 8-row group, physical chunk lane & 7
   const int lrow = lane >> 3, pc = lane & 7;
+  char* const gsm = smem + grp * SLOT;  // this key group's share of each ring slot
   auto issue = [&](int kt, int slot) {
-    char* sK = smem + slot * SLOT;
+    char* sK = gsm + slot * NS * SLOT;
     char* sV = sK + TILE_B;
 #pragma unroll
     for (int i = 0; i < INS; ++i) {
@@ -306,7 +325,7 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
   using Q1 = std::integral_constant<int, QS - 1>;
   auto tile = [&](int kt, auto slot_tag, auto first_tag) {
     constexpr int slot = decltype(slot_tag)::value;  // compile-time: LDS offsets fold into ds_read immediates
-    const char* K_ = smem + slot * SLOT;
+    const char* K_ = gsm + slot * NS * SLOT;
     {
       const Scores sc = scores(K_, kt, 0, first_tag);
       softmax_pv(Q0{}, sc.v[0], K_ + TILE_B, 0, first_tag);
@@ -327,7 +346,7 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
   auto step = [&](int kt, auto slot_tag, auto first_tag) {
     constexpr int SL = decltype(slot_tag)::value;
     if (kt + DIST < kt1) issue(kt + DIST, (SL + DIST) % R);
-    if (active) tile(kt, slot_tag, first_tag);
+    if (active && (NS == 1 || kt < kt1)) tile(kt, slot_tag, first_tag);
     wait_tiles(min(kt1 - 1, kt + DIST) - (kt + 1));
     lds_barrier();
   };
@@ -337,15 +356,64 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
   using S3 = std::integral_constant<int, 3 % R>;
   step(kt0, S0{}, std::true_type{});
   int kt = kt0 + 1;
-  for (; kt + R <= kt1; kt += R) {
+  for (; kt + R <= ktl; kt += R) {
     step(kt, S1{}, NF{});
     step(kt + 1, S2{}, NF{});
     if constexpr (R > 2) step(kt + 2, S3{}, NF{});
     if constexpr (R > 3) step(kt + 3, S0{}, NF{});
   }
-  if (kt < kt1) step(kt, S1{}, NF{});
-  if (R > 2 && kt + 1 < kt1) step(kt + 1, S2{}, NF{});
-  if (R > 3 && kt + 2 < kt1) step(kt + 2, S3{}, NF{});
+  if (kt < ktl) step(kt, S1{}, NF{});
+  if (R > 2 && kt + 1 < ktl) step(kt + 1, S2{}, NF{});
+  if (R > 3 && kt + 2 < ktl) step(kt + 2, S3{}, NF{});
+
+  if constexpr (NS > 1) {
+    // merge the key groups: groups 1.. park (O^T, m, l) in LDS (the ring is
+    // free: every wave's last LDS read came before the last step's barrier,
+    // and that step waited out every load), group 0 rescales to the common
+    // max and sums.  Lane layout is identical across groups (same queries).
+    // An empty group (kt0 >= nkt_all: tiny T) is skipped.
+    float* mb = reinterpret_cast<float*>(smem);
+    if (grp > 0) {
+      float* w = mb + ((grp - 1) * NWQ + wave) * (MERGE_WAVE_B / 4);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const f32x16& a = acc[0][c >> 2];
+        *reinterpret_cast<float4*>(w + (c * 64 + lane) * 4) =
+            make_float4(a[4 * (c & 3)], a[4 * (c & 3) + 1], a[4 * (c & 3) + 2], a[4 * (c & 3) + 3]);
+      }
+      *reinterpret_cast<float2*>(w + 8 * 64 * 4 + lane * 2) = make_float2(m_run[0], l_run[0]);
+    }
+    __syncthreads();
+    if (grp > 0) return;
+    float mg[NS];
+    mg[0] = m_run[0];
+    float mmax = m_run[0];
+#pragma unroll
+    for (int g = 1; g < NS; ++g) {
+      const float* w = mb + ((g - 1) * NWQ + wave) * (MERGE_WAVE_B / 4);
+      mg[g] = w[8 * 64 * 4 + lane * 2];
+      if (g * gper < nkt_all) mmax = fmaxf(mmax, mg[g]);
+    }
+    const float a0 = __builtin_amdgcn_exp2f(m_run[0] - mmax);
+    l_run[0] *= a0;
+    acc[0][0] *= a0;
+    acc[0][1] *= a0;
+#pragma unroll
+    for (int g = 1; g < NS; ++g) {
+      if (g * gper >= nkt_all) continue;  // wave-uniform
+      const float* w = mb + ((g - 1) * NWQ + wave) * (MERGE_WAVE_B / 4);
+      const float ag = __builtin_amdgcn_exp2f(mg[g] - mmax);
+      l_run[0] += ag * w[8 * 64 * 4 + lane * 2 + 1];
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float4 v = *reinterpret_cast<const float4*>(w + (c * 64 + lane) * 4);
+        acc[0][c >> 2][4 * (c & 3)] += ag * v.x;
+        acc[0][c >> 2][4 * (c & 3) + 1] += ag * v.y;
+        acc[0][c >> 2][4 * (c & 3) + 2] += ag * v.z;
+        acc[0][c >> 2][4 * (c & 3) + 3] += ag * v.w;
+      }
+    }
+  }
   if (!active) return;
 
   if constexpr (SPLIT) {
@@ -465,6 +533,18 @@ hipError_t run_attn(const h16* q, const h16* k, const h16* vt, h16* o, int B, in
   return hipGetLastError();
 }
 
+// NS key groups of NW / NS query waves in each workgroup (in-workgroup split-KV)
+template <int NW, int NS>
+hipError_t run_attn_grp(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T, int Tpad, int ldo,
+                        hipStream_t st) {
+  constexpr int BQ = QW * (NW / NS);
+  const int nqb = (T + BQ - 1) / BQ;
+  hipLaunchKernelGGL((attn_fwd_kernel<NW, false, 2, 1, NS>), dim3(nqb, B * H), dim3(NW * 64), 0, st,
+                     reinterpret_cast<const f16*>(q), reinterpret_cast<const f16*>(k), reinterpret_cast<const f16*>(vt),
+                     reinterpret_cast<f16*>(o), H, T, Tpad, ldo, SplitWs{});
+  return hipGetLastError();
+}
+
 }  // namespace
 
 size_t attention_split_ws_bytes(int B, int H, int T) {
@@ -474,14 +554,15 @@ size_t attention_split_ws_bytes(int B, int H, int T) {
 }
 
 hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T, int Tpad,
-                            int ldo, hipStream_t st, float* ws, size_t ws_bytes) {
+                            int ldo, hipStream_t st, float* ws, size_t ws_bytes, const char* cfg) {
   if (B <= 0 || T <= 0) return hipSuccess;
   // the 16-B output stores need ldo % 8 == 0 (and a 16-B aligned o)
   if (Tpad % KT || Tpad < ((T + KT - 1) / KT) * KT || (ldo & 7) || ((uintptr_t)o & 15)) return hipErrorInvalidValue;
   const int nkt = (T + KT - 1) / KT;
   // MDE_ATTN_CFG = <waves>[s<split>][r<ring>] ("8", "4", "4s8", "8r3", ...): tuning override
-  static const char* forced = getenv("MDE_ATTN_CFG");
-  int nw = 0, split = 1, ring = ATTN_RING, qs2 = 0;
+  static const char* env_cfg = getenv("MDE_ATTN_CFG");
+  const char* forced = cfg && cfg[0] ? cfg : env_cfg;
+  int nw = 0, split = 1, ring = ATTN_RING, qs2 = 0, groups = 1;
   if (forced) {
     nw = atoi(forced);
     const char* sp = strchr(forced, 's');
@@ -489,6 +570,14 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
     const char* rp = strchr(forced, 'r');
     if (rp) ring = atoi(rp + 1);
     qs2 = strstr(forced, "q2") != nullptr;
+    const char* gp = strchr(forced, 'g');  // "<waves>g<groups>": in-workgroup key groups
+    if (gp) groups = atoi(gp + 1);
+  }
+  if (groups > 1 && nkt >= groups) {
+    if (nw == 4 && groups == 2) return run_attn_grp<4, 2>(q, k, vt, o, B, H, T, Tpad, ldo, st);
+    if (nw == 4 && groups == 4) return run_attn_grp<4, 4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
+    if (nw == 8 && groups == 2) return run_attn_grp<8, 2>(q, k, vt, o, B, H, T, Tpad, ldo, st);
+    if (nw == 8 && groups == 4) return run_attn_grp<8, 4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
   }
   if (nw != 4 && nw != 8) {
     // 256-query workgroups share each K/V^T tile over 8 waves once the grid

@@ -165,6 +165,18 @@ bool lnfold_off() {
   return off;
 }
 
+// Fork the DPT reassemble + layerN_rn work of taps 0..2 onto a side stream
+// while the encoder's remaining blocks run, when the encoder's launches leave
+// the chip under-filled: at most ~2 workgroups per CU in its widest GEMM
+// (128^2 tiles of the MLP's first linear).  MDE_DPT_FORK=0 / 1 overrides
+// (read per forward: tests toggle it; a captured graph keeps its choice).
+bool dpt_fork(const mde_engine& e, int B) {
+  const char* s = getenv("MDE_DPT_FORK");
+  if (s && s[0]) return s[0] == '1';
+  const long long tiles = (long long)((B * e.T + 127) / 128) * ((e.cfg.mlp_hidden + 127) / 128);
+  return tiles <= 512;
+}
+
 size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
   ArenaPlan a(base);
   const size_t bb = (size_t)B;
@@ -218,6 +230,7 @@ size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
   t.aws_bytes = bsplit >= 1 ? attention_split_ws_bytes(bsplit, e.H, e.T) : 0;
   t.aws = t.aws_bytes ? a.f(t.aws_bytes / sizeof(float)) : nullptr;
   t.sws = a.f(kSplitWsFloats);
+  t.sws2 = a.f(kSplitWsFloats);
   if (b) *b = t;
   return a.off;
 }
@@ -293,8 +306,75 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
     }
     gemm("patch_embed", g);
   }
-  int tap = 0;
+  // ---- DPT head: reassemble (project, resize layer) + layerN_rn of tap i ----
+  const int hs[4] = {4 * e.ph, 2 * e.ph, e.ph, e.h4};
+  const int ws[4] = {4 * e.pw, 2 * e.pw, e.pw, e.w4};
+  const h16* lay[4] = {b.l1, b.l2, b.pj[2], b.l4};
+  const int cin[4] = {e.c1p, oc[1], oc[2], oc[3]};
   char nm[64];
+  auto reassemble = [&](int i) {
+    {
+      GemmParams g = dense(b.tap[i], D, "proj" + std::to_string(i) + ".w", B * np, oc[i], D);
+      g.emode = E_STORE;
+      g.bias = w32("proj" + std::to_string(i) + ".b");
+      g.out16 = b.pj[i];
+      g.ldo = oc[i];
+      snprintf(nm, sizeof nm, "reassemble%d.project", i);
+      gemm(nm, g);
+    }
+    if (i == 0) {
+      GemmParams g = dense(b.pj[0], oc[0], "rs0.w", B * np, 16 * oc[0], oc[0]);
+      g.emode = E_CONVT;
+      g.bias = w32("rs0.b");
+      g.out16 = b.l1;
+      g.s = 4;
+      g.cout = oc[0];
+      g.ldo = e.c1p;
+      g.ih = e.ph;
+      g.iw = e.pw;
+      gemm("reassemble0.convT4", g);
+    } else if (i == 1) {
+      GemmParams g = dense(b.pj[1], oc[1], "rs1.w", B * np, 4 * oc[1], oc[1]);
+      g.emode = E_CONVT;
+      g.bias = w32("rs1.b");
+      g.out16 = b.l2;
+      g.s = 2;
+      g.cout = oc[1];
+      g.ldo = oc[1];
+      g.ih = e.ph;
+      g.iw = e.pw;
+      gemm("reassemble1.convT2", g);
+    } else if (i == 3) {
+      GemmParams g = conv(b.pj[3], B, e.ph, e.pw, oc[3], "rs3.w", oc[3], 2);
+      g.bias = w32("rs3.b");
+      g.out16 = b.l4;
+      gemm("reassemble3.conv_s2", g);
+    }
+    GemmParams g = conv(lay[i], B, hs[i], ws[i], cin[i], "rn" + std::to_string(i + 1) + ".w", F, 1);
+    g.out16 = b.rn[i];
+    snprintf(nm, sizeof nm, "layer%d_rn", i + 1);
+    gemm(nm, g);
+  };
+  // Small grids: taps 0..2's reassemble branch runs on the side stream
+  // beside the encoder's later blocks (it reads only its tap map and writes
+  // only its own buffers; its split-K partials go to sws2), joined before
+  // the tap-3 branch and the fusion blocks.  Not under the per-layer
+  // profiler (one stream, so layer times stay attributable).
+  const bool fork = !prof && c.side_stream && b.sws2 && dpt_fork(e, B);
+  auto fork_reassemble = [&](int i) {
+    if (err != hipSuccess) return;
+    if ((err = hipEventRecord(c.fork_ev[i], st)) != hipSuccess) return;
+    if ((err = hipStreamWaitEvent(c.side_stream, c.fork_ev[i], 0)) != hipSuccess) return;
+    const hipStream_t main_st = st;
+    float* const main_ws = split_ws;
+    st = c.side_stream;
+    split_ws = b.sws2;
+    reassemble(i);
+    st = main_st;
+    split_ws = main_ws;
+  };
+
+  int tap = 0;
   for (int i = 0; i < cf.depth; ++i) {
     const std::string p = "b" + std::to_string(i) + ".";
     const std::string pn = "b" + std::to_string(i + 1) + ".";
@@ -404,60 +484,17 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
       step(nm, [&] {
         return launch_layernorm(b.X, dst, w32("norm.g"), w32("norm.b"), B * T, D, cf.ln_eps, T, 1, st, b.Xh);
       });
+      if (fork && tap < 3) fork_reassemble(tap);
       ++tap;
     }
   }
   if (tap != 4) return hipErrorInvalidValue;
-
-  // ---- DPT head: reassemble ----
-  for (int i = 0; i < 4; ++i) {
-    GemmParams g = dense(b.tap[i], D, "proj" + std::to_string(i) + ".w", B * np, oc[i], D);
-    g.emode = E_STORE;
-    g.bias = w32("proj" + std::to_string(i) + ".b");
-    g.out16 = b.pj[i];
-    g.ldo = oc[i];
-    snprintf(nm, sizeof nm, "reassemble%d.project", i);
-    gemm(nm, g);
-  }
-  {
-    GemmParams g = dense(b.pj[0], oc[0], "rs0.w", B * np, 16 * oc[0], oc[0]);
-    g.emode = E_CONVT;
-    g.bias = w32("rs0.b");
-    g.out16 = b.l1;
-    g.s = 4;
-    g.cout = oc[0];
-    g.ldo = e.c1p;
-    g.ih = e.ph;
-    g.iw = e.pw;
-    gemm("reassemble0.convT4", g);
-  }
-  {
-    GemmParams g = dense(b.pj[1], oc[1], "rs1.w", B * np, 4 * oc[1], oc[1]);
-    g.emode = E_CONVT;
-    g.bias = w32("rs1.b");
-    g.out16 = b.l2;
-    g.s = 2;
-    g.cout = oc[1];
-    g.ldo = oc[1];
-    g.ih = e.ph;
-    g.iw = e.pw;
-    gemm("reassemble1.convT2", g);
-  }
-  {
-    GemmParams g = conv(b.pj[3], B, e.ph, e.pw, oc[3], "rs3.w", oc[3], 2);
-    g.bias = w32("rs3.b");
-    g.out16 = b.l4;
-    gemm("reassemble3.conv_s2", g);
-  }
-  const int hs[4] = {4 * e.ph, 2 * e.ph, e.ph, e.h4};
-  const int ws[4] = {4 * e.pw, 2 * e.pw, e.pw, e.w4};
-  const h16* lay[4] = {b.l1, b.l2, b.pj[2], b.l4};
-  const int cin[4] = {e.c1p, oc[1], oc[2], oc[3]};
-  for (int i = 0; i < 4; ++i) {
-    GemmParams g = conv(lay[i], B, hs[i], ws[i], cin[i], "rn" + std::to_string(i + 1) + ".w", F, 1);
-    g.out16 = b.rn[i];
-    snprintf(nm, sizeof nm, "layer%d_rn", i + 1);
-    gemm(nm, g);
+  if (fork) {
+    if (err == hipSuccess) err = hipEventRecord(c.join_ev, c.side_stream);
+    if (err == hipSuccess) err = hipStreamWaitEvent(st, c.join_ev, 0);
+    reassemble(3);
+  } else {
+    for (int i = 0; i < 4; ++i) reassemble(i);
   }
   // ---- fusion (refinenet4 .. refinenet1) ----
   dav2_fusion(4, b.rn[3], nullptr, B, hs[3], ws[3], b.p4, hs[2], ws[2]);
@@ -748,6 +785,9 @@ int mde_context_create(mde_engine* e, int max_batch, mde_context** out) {
   // zero once: the q/k/v^T pad rows/columns beyond T must stay 0
   he = hipMemset(c->arena, 0, c->arena_bytes);
   if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking);
+  if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking);
+  for (int i = 0; i < 3 && he == hipSuccess; ++i) he = hipEventCreateWithFlags(&c->fork_ev[i], hipEventDisableTiming);
+  if (he == hipSuccess) he = hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming);
   if (he == hipSuccess) he = hipDeviceSynchronize();
   if (he != hipSuccess) {
     hipFree(c->arena);
@@ -771,6 +811,10 @@ int mde_context_destroy(mde_context* c) {
     hipEventDestroy(pe.second.second);
   }
   if (c->cap_stream) hipStreamDestroy(c->cap_stream);
+  if (c->side_stream) hipStreamDestroy(c->side_stream);
+  for (hipEvent_t ev : c->fork_ev)
+    if (ev) hipEventDestroy(ev);
+  if (c->join_ev) hipEventDestroy(c->join_ev);
   if (c->arena) hipFree(c->arena);
   delete c;
   return MDE_OK;
@@ -1235,6 +1279,14 @@ int mde_op_attention_ws(const void* q, const void* k, const void* vt, void* o, i
   OP_RET(launch_attention((const h16*)q, (const h16*)k, (const h16*)vt, (h16*)o, batch, heads, tokens, tokens_pad,
                           ldo, (hipStream_t)st, (float*)ws, ws_bytes),
          "attention_ws");
+}
+
+int mde_op_attention_cfg(const void* q, const void* k, const void* vt, void* o, int batch, int heads, int tokens,
+                         int tokens_pad, int ldo, const char* cfg, void* ws, size_t ws_bytes, void* st) {
+  if (!q || !k || !vt || !o || (!ws && ws_bytes)) return fail(MDE_ERR_ARG, "null argument");
+  OP_RET(launch_attention((const h16*)q, (const h16*)k, (const h16*)vt, (h16*)o, batch, heads, tokens, tokens_pad,
+                          ldo, (hipStream_t)st, (float*)ws, ws_bytes, cfg),
+         "attention_cfg");
 }
 
 size_t mde_op_attention_ws_bytes(int batch, int heads, int tokens) {

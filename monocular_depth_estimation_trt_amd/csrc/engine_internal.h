@@ -39,6 +39,7 @@ struct DAV2Buf {
   size_t aws_bytes;
   float* st;        // folded-LN partials [B*T][D/32][2] (f16 residual + folded pack, else null)
   float* sws;       // E_STORE split-K partials (GemmParams::partial_cap = kSplitWsFloats)
+  float* sws2;      // the same for the reassemble branch forked onto the side stream
 };
 
 // fp32 elements of a context's E_STORE split-K workspace (launch_gemm bounds
@@ -140,6 +141,12 @@ struct mde_context {
   mde::VGBuf v{};
   bool graph_mode = true;
   hipStream_t cap_stream = nullptr;
+  // DPT reassemble branch of taps 0..2 forked off the encoder (small grids):
+  // a second stream + fork / join events (captured into the graph as a
+  // parallel branch)
+  hipStream_t side_stream = nullptr;
+  hipEvent_t fork_ev[3] = {nullptr, nullptr, nullptr};
+  hipEvent_t join_ev = nullptr;
   // captured forwards per (batch, io addresses), at most kMaxGraphs of them:
   // the least recently launched one is destroyed to make room (a caller that
   // rebinds fresh buffers every call pays a capture, not unbounded growth)

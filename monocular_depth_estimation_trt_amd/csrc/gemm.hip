@@ -492,6 +492,7 @@ int tile_override() {
     if (!strcmp(e, "256x128")) return 2;
     if (!strcmp(e, "128x256")) return 3;
     if (!strcmp(e, "256x128w8")) return 4;  // 8 waves, BK 32 x 3 stages, two workgroups per CU
+    if (!strcmp(e, "128x128w8")) return 5;  // 8 waves (2 x 4 of 64 x 32) on the 128^2 tile, any grid
     return 0;
   }();
   return v;
@@ -523,6 +524,7 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
     // 256 x 128 tiles on 8 waves (4 x 2 of 64 x 64), BK 32 x 3 stages = 72 KB:
     // two workgroups per CU, 25 % fewer L2 -> LDS bytes per FLOP than 128^2
     if (tile_override() == 4 && p.M >= 256 && p.N >= 128) return run<256, 128, 4, 2, AM, EM, 32>(p, st);
+    if (tile_override() == 5 && p.N >= 128) return run<128, 128, 2, 4, AM, EM>(p, st);
   }
   if constexpr (EM == E_HEAD) {
     return run<128, 32, 4, 1, AM, EM>(p, st);
@@ -694,7 +696,10 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
     q.bias = nullptr;
     q.ls = nullptr;
     q.lnst_out = nullptr;  // the reduce kernel writes the LN partials
-    if (big) {
+    if (big && tile_override() == 5) {
+      hipLaunchKernelGGL((gemm_kernel<128, 128, MDE_GEMM_BK, 2, 4, A_DENSE, E_PARTIAL>), dim3((unsigned)t128, (unsigned)S),
+                         dim3(512), 0, st, q);
+    } else if (big) {
       hipLaunchKernelGGL((gemm_kernel<128, 128, MDE_GEMM_BK, 2, 2, A_DENSE, E_PARTIAL>), dim3((unsigned)t128, (unsigned)S),
                          dim3(256), 0, st, q);
     } else {

@@ -110,8 +110,11 @@ hipError_t launch_gemm256(const GemmParams& p, hipStream_t st);
 
 // ws (optional, attention_split_ws_bytes): fp32 workspace for the split-KV
 // path the launcher takes on grids too small to fill the chip (batch 1)
+// cfg (optional) = the MDE_ATTN_CFG syntax ("8", "4s2", "4g2", ...): forces a
+// workgroup shape / split for tests and tuning; nullptr = env, then the policy.
 hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T,
-                            int Tpad, int ldo, hipStream_t st, float* ws = nullptr, size_t ws_bytes = 0);
+                            int Tpad, int ldo, hipStream_t st, float* ws = nullptr, size_t ws_bytes = 0,
+                            const char* cfg = nullptr);
 size_t attention_split_ws_bytes(int B, int H, int T);
 
 // x (fp32) or xh (f16) residual rows -> LayerNorm -> f16 y

@@ -171,8 +171,9 @@ def test_batch_and_graph_consistency(gpu):
 
 @pytest.mark.parametrize("encoder,size", [("vits", 98), ("vitl", 518)])
 def test_fc2_splitk_matches_unsplit(gpu, encoder, size):
-    """Small-batch contexts split fc2's K loop (engine.hip split_k: ViT-S at
-    98^2 4 slices, ViT-L at 518^2 2 slices -- config 3's B=1); the slices are
+    """Small-batch contexts split fc2's K loop (gemm.hip launch_gemm: ViT-S at
+    98^2 4 slices of 64^2 tiles, ViT-L at 518^2 4 slices of 128^2 tiles --
+    config 3's B=1); the slices are
     summed in order, so the result is deterministic and equal to the unsplit
     GEMM up to fp32 reassociation."""
     cfg = weights.model_config(encoder, "metric")
@@ -191,6 +192,30 @@ def test_fc2_splitk_matches_unsplit(gpu, encoder, size):
     # the fp32 reassociation is amplified by the downstream f16 roundings
     # (measured ViT-S 0.026 m / 6.6e-4, ViT-L 0.036 m / 6.2e-4)
     assert m["max_abs"] < 0.08 and m["rel_mean"] < 1.5e-3, m
+
+
+@pytest.mark.parametrize("encoder,size,B", [("vits", 98, 2), ("vitl", 518, 1)])
+def test_dpt_fork_bit_exact(gpu, encoder, size, B):
+    """Small grids run the reassemble + layerN_rn branch of taps 0..2 on a
+    side stream beside the encoder's later blocks (engine.hip dpt_fork, a
+    parallel branch of the captured graph).  Only the launch order changes:
+    the depth map must equal the one-stream forward bit for bit, in graph
+    replay and eager mode."""
+    cfg = weights.model_config(encoder, "metric")
+    sd = weights.synthetic_state_dict(cfg, 8)
+    blob = pack.pack_bytes(sd, cfg, size, size)
+    x = weights.synthetic_images(B, size, size, first_seed=31)
+    os.environ["MDE_DPT_FORK"] = "1"
+    try:
+        y_fork = run_engine(blob, x, graph=True)
+        y_fork_eager = run_engine(blob, x, graph=False)
+        os.environ["MDE_DPT_FORK"] = "0"
+        y_one = run_engine(blob, x, graph=True)
+    finally:
+        os.environ.pop("MDE_DPT_FORK", None)
+    assert np.isfinite(y_one).all()
+    assert np.array_equal(y_fork, y_one), "forked DPT branch (graph) must equal the one-stream forward"
+    assert np.array_equal(y_fork_eager, y_one), "forked DPT branch (eager) must equal the one-stream forward"
 
 
 @pytest.mark.parametrize("encoder", ["vits", "vitl"])

@@ -151,6 +151,33 @@ def test_attention_split_kv(gpu, B, H, T, spiky):
     close(o, ref, 2e-2, 5e-3, f"attention split-KV B{B} H{H} T{T}")
 
 
+@pytest.mark.parametrize("cfg", ["4g2", "8g2", "4g4", "8g4"])
+@pytest.mark.parametrize("B,H,T,spiky", [(1, 16, 1370, False), (1, 6, 1370, True), (2, 3, 129, False),
+                                         (1, 2, 300, True), (1, 1, 200, False)])
+def test_attention_key_groups(gpu, cfg, B, H, T, spiky):
+    """In-workgroup split-KV (attention.hip, NS key groups of NW / NS query
+    waves merged through LDS): uneven group lengths (T 129: 2 + 1 tiles),
+    an empty group (T 300 at 4 groups: 2 + 2 + 1 + 0 tiles), the partial last
+    tile, and dominant keys in different groups (spiky)."""
+    Tp = -(-T // 64) * 64
+    q = rn(B * H, T, 64) * 0.125 * 2.0 * LOG2E
+    k = rn(B * H, T, 64) * 2.0
+    if spiky:
+        k[:, T - 10] = q.mean(1) * 60.0
+        k[:, 3] = q.mean(1) * 30.0
+    v = rn(B * H, T, 64)
+    ref = attn_ref(q, k, v).reshape(B, H, T, 64).permute(0, 2, 1, 3).reshape(B * T, H * 64)
+    qg = torch.zeros(B * H, Tp, 64, dtype=torch.float16, device=gpu)
+    kg = torch.zeros_like(qg)
+    vtg = torch.zeros(B * H, 64, Tp, dtype=torch.float16, device=gpu)
+    qg[:, :T], kg[:, :T] = q.half().to(gpu), k.half().to(gpu)
+    vtg[:, :, vt_perm(T).to(gpu)] = v.transpose(1, 2).half().to(gpu)
+    o = torch.empty(B * T, H * 64, dtype=torch.float16, device=gpu)
+    op("mde_op_attention_cfg", ptr(qg), ptr(kg), ptr(vtg), ptr(o), B, H, T, Tp, H * 64, cfg.encode(), None, 0,
+       stream())
+    close(o, ref, 2e-2, 5e-3, f"attention {cfg} B{B} H{H} T{T}")
+
+
 def test_attention_spiky_rows(gpu):
     """Force the online-softmax rescale: one key dominates late in the row."""
     B, H, T = 1, 2, 300

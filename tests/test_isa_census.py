@@ -1,6 +1,6 @@
 """Static instruction census of the attention kernel's hot loop (CPU only:
 hipcc cross-compiles gfx950 here).  Guards the VALU budget per MFMA that the
-r02 verdict set for the B = 48 kernel (attn_fwd_kernel<8, false, 2, 1>):
+r02 verdict set for the B = 48 kernel (attn_fwd_kernel<8, false, 2, 1, 1>):
 the softmax of one 32-key block -- 8 row-max, 16 exp2, 8 f16 packs, 16
 row-sum adds -- against its 8 v_mfma_f32_32x32x16_f16 (4 for S^T = K Q^T, 4
 for O^T += V^T P^T), i.e. <= 6.5 VALU and exactly 2 transcendentals per
@@ -21,7 +21,7 @@ def test_attention_hot_loop_valu_per_mfma():
     import isa_census
     dis = isa_census.disassemble(os.path.join(ROOT, "monocular_depth_estimation_trt_amd", "csrc", "attention.hip"))
     ks = isa_census.kernels(dis)
-    name = next(k for k in ks if "attn_fwd_kernelILi8ELb0ELi2ELi1E" in k)
+    name = next(k for k in ks if "attn_fwd_kernelILi8ELb0ELi2ELi1ELi1EE" in k)
     res = isa_census.analyse(ks[name])
     hot = res["hot_path"]
     assert hot["classes"]["mfma"] % 8 == 0 and hot["classes"]["mfma"] >= 16, hot

@@ -155,7 +155,7 @@ def analyse(insts):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--src", default=os.path.join(ROOT, "monocular_depth_estimation_trt_amd", "csrc", "attention.hip"))
-    ap.add_argument("--kernel", default="attn_fwd_kernelILi8ELb0ELi2ELi1E")
+    ap.add_argument("--kernel", default="attn_fwd_kernelILi8ELb0ELi2ELi1ELi1EE")
     ap.add_argument("--json", default="")
     a = ap.parse_args()
     ks = kernels(disassemble(a.src))
