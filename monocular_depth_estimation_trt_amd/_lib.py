@@ -151,6 +151,17 @@ def lib() -> C.CDLL:
                     f"libmde_hip.so not found at {LIB_PATH}. Build it first: "
                     f"python -c 'import __graft_entry__ as g; g.build()' (or "
                     f"python -m monocular_depth_estimation_trt_amd._build). There is no CPU fallback.")
+            # PyTorch-ROCm wheels bundle their own libamdhip64: with two HIP
+            # runtimes in one process, ours finds no device when it is loaded
+            # before torch's runtime has come up and initialised after it
+            # (measured on the MI355X box: build() then smoke() in one process
+            # failed hipSetDevice; torch first, or ours loaded after torch's
+            # init, works).  Bring torch's runtime up first when torch is here.
+            try:
+                import torch
+                torch.cuda.is_available()
+            except ImportError:
+                pass
             L = C.CDLL(LIB_PATH)
             for name, args in PROTOTYPES.items():
                 f = getattr(L, name)

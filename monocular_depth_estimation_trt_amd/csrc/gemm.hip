@@ -100,9 +100,11 @@ struct KGeo {
 // BK 32 (the short-K 128^2 dense stores): 3-stage ring = 48 KB and a half-size
 // epilogue staging, capped at 168 VGPRs -- three workgroups per CU, so one
 // workgroup's epilogue stores overlap the others' main loops
-template <int BM, int BN, int BK, int WM, int WN, int AM, int EM>
+// STG > 0: ring depth forced (small grids: one workgroup per CU with
+// STG - 1 K-steps in flight instead of two workgroups with one each)
+template <int BM, int BN, int BK, int WM, int WN, int AM, int EM, int STG = 0>
 __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
-    __attribute__((amdgpu_waves_per_eu(BK == 32 ? (WM * WN == 8 ? 4 : (MDE_BK32_STAGES > 2 ? 3 : 4)) : 1)))
+    __attribute__((amdgpu_waves_per_eu(STG == 0 && BK == 32 ? (WM * WN == 8 ? 4 : (MDE_BK32_STAGES > 2 ? 3 : 4)) : 1)))
     gemm_kernel(const GemmParams p) {
   using G = KGeo<BK>;
   constexpr int ROWB = G::ROWB, CH = G::CH;
@@ -119,7 +121,7 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
   constexpr int STAGE = (BM + BN) * ROWB;
   // dense A: SG-deep ring, every wave issues exactly NPER glds per stage so a
   // counted vmcnt names "stage kt has landed"
-  constexpr int SGWANT = BK == 32 ? MDE_BK32_STAGES : MDE_GEMM_STAGES;
+  constexpr int SGWANT = STG > 0 ? STG : (BK == 32 ? MDE_BK32_STAGES : MDE_GEMM_STAGES);
   constexpr int SGMAX = 163840 / STAGE < SGWANT ? 163840 / STAGE : SGWANT;  // LDS limit
   constexpr int SG = (AM == A_DENSE && AINS % NW == 0 && BINS % NW == 0 && SGMAX > 2) ? SGMAX : 2;
   constexpr int NPER = APASS + BPASS;
@@ -456,12 +458,12 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
   }
   if (!staged) store_tile<EM, TM, TN>(p, acc, mrow, n0 + wn * TN * 16 + (lane >> 4) * 4, lane);
 }
-template <int BM, int BN, int WM, int WN, int AM, int EM, int BKSEL = MDE_GEMM_BK>
+template <int BM, int BN, int WM, int WN, int AM, int EM, int BKSEL = MDE_GEMM_BK, int STG = 0>
 hipError_t run(const GemmParams& p, hipStream_t st) {
   const int gm = (p.M + BM - 1) / BM, gn = (p.N + BN - 1) / BN;
   const long long blocks = (long long)gm * gn;
   if (blocks <= 0) return hipSuccess;
-  hipLaunchKernelGGL((gemm_kernel<BM, BN, BKSEL, WM, WN, AM, EM>), dim3((unsigned)blocks), dim3(WM * WN * 64), 0,
+  hipLaunchKernelGGL((gemm_kernel<BM, BN, BKSEL, WM, WN, AM, EM, STG>), dim3((unsigned)blocks), dim3(WM * WN * 64), 0,
                      st, p);
   return hipGetLastError();
 }
@@ -484,8 +486,9 @@ bool bk32_tiles() {
 }
 
 // tuning override for large dense problems: MDE_GEMM_TILE = 256x256 | 256x128 | 128x256
+// (read per launch: tests toggle it; a captured graph keeps its choice)
 int tile_override() {
-  static const int v = [] {
+  {
     const char* e = getenv("MDE_GEMM_TILE");
     if (!e) return 0;
     if (!strcmp(e, "256x256")) return 1;
@@ -493,9 +496,9 @@ int tile_override() {
     if (!strcmp(e, "128x256")) return 3;
     if (!strcmp(e, "256x128w8")) return 4;  // 8 waves, BK 32 x 3 stages, two workgroups per CU
     if (!strcmp(e, "128x128w8")) return 5;  // 8 waves (2 x 4 of 64 x 32) on the 128^2 tile, any grid
+    if (!strcmp(e, "big1")) return 6;       // small grids: tall tiles, 3-deep ring, one workgroup per CU
     return 0;
-  }();
-  return v;
+  }
 }
 
 // 128^2 tiles once the grid holds at least this many of them (MDE_GEMM_BIG_MIN: tuning)
@@ -525,6 +528,20 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
     // two workgroups per CU, 25 % fewer L2 -> LDS bytes per FLOP than 128^2
     if (tile_override() == 4 && p.M >= 256 && p.N >= 128) return run<256, 128, 4, 2, AM, EM, 32>(p, st);
     if (tile_override() == 5 && p.N >= 128) return run<128, 128, 2, 4, AM, EM>(p, st);
+    if constexpr (EM == E_STORE || EM == E_QKV) {
+      // small grids (under one 128^2 tile per CU... up to ~1.4): the tallest
+      // row block that keeps the grid within one workgroup per CU, on a
+      // 3-deep ring (2 K-steps, 72-80 KB, in flight per CU)
+      if (tile_override() == 6 && p.N >= 128 && !p.lnst_out) {
+        const long long gn = (p.N + 127) / 128;
+        const long long t128 = (long long)((p.M + 127) / 128) * gn;
+        if (t128 < 512) {
+          if (t128 <= 256) return run<128, 128, 2, 2, AM, EM, 64, 3>(p, st);
+          if ((long long)((p.M + 159) / 160) * gn <= 256) return run<160, 128, 2, 2, AM, EM, 64, 3>(p, st);
+          if ((long long)((p.M + 191) / 192) * gn <= 256) return run<192, 128, 2, 2, AM, EM, 64, 3>(p, st);
+        }
+      }
+    }
   }
   if constexpr (EM == E_HEAD) {
     return run<128, 32, 4, 1, AM, EM>(p, st);
@@ -696,7 +713,11 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
     q.bias = nullptr;
     q.ls = nullptr;
     q.lnst_out = nullptr;  // the reduce kernel writes the LN partials
-    if (big && tile_override() == 5) {
+    const long long t192 = (long long)((p.M + 191) / 192) * ((p.N + 127) / 128);
+    if (big && tile_override() == 6 && t192 * 4 <= 256) {
+      hipLaunchKernelGGL((gemm_kernel<192, 128, MDE_GEMM_BK, 2, 2, A_DENSE, E_PARTIAL, 3>),
+                         dim3((unsigned)t192, (unsigned)S), dim3(256), 0, st, q);
+    } else if (big && tile_override() == 5) {
       hipLaunchKernelGGL((gemm_kernel<128, 128, MDE_GEMM_BK, 2, 4, A_DENSE, E_PARTIAL>), dim3((unsigned)t128, (unsigned)S),
                          dim3(512), 0, st, q);
     } else if (big) {

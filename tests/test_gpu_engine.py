@@ -218,6 +218,27 @@ def test_dpt_fork_bit_exact(gpu, encoder, size, B):
     assert np.array_equal(y_fork_eager, y_one), "forked DPT branch (eager) must equal the one-stream forward"
 
 
+@pytest.mark.parametrize("tile", ["big1", "128x128w8"])
+def test_gemm_tile_variants_bit_exact(gpu, tile):
+    """ViT-L 518^2 B=1 (config 3's unit) with the small-grid GEMM tilings
+    (MDE_GEMM_TILE: tall 160/192-row tiles on a 3-deep ring, or 8 waves on
+    the 128^2 tile).  A tile's K loop runs in the same order whatever its
+    shape and the split-K slicing is unchanged, so the depth map must equal
+    the default tiling's bit for bit."""
+    cfg = weights.model_config("vitl", "metric")
+    sd = weights.synthetic_state_dict(cfg, 12)
+    blob = pack.pack_bytes(sd, cfg, 518, 518)
+    x = weights.synthetic_images(1, 518, 518, first_seed=51)
+    y_def = run_engine(blob, x)
+    os.environ["MDE_GEMM_TILE"] = tile
+    try:
+        y_var = run_engine(blob, x)
+    finally:
+        os.environ.pop("MDE_GEMM_TILE", None)
+    assert np.isfinite(y_def).all()
+    assert np.array_equal(y_var, y_def), f"MDE_GEMM_TILE={tile} changed the result"
+
+
 @pytest.mark.parametrize("encoder", ["vits", "vitl"])
 def test_fp32_precision_engine_vs_golden_518(gpu, encoder):
     """precision "fp32" (get_engine's reference default): the residual stream
