@@ -573,12 +573,6 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
     const char* gp = strchr(forced, 'g');  // "<waves>g<groups>": in-workgroup key groups
     if (gp) groups = atoi(gp + 1);
   }
-  if (groups > 1 && nkt >= groups) {
-    if (nw == 4 && groups == 2) return run_attn_grp<4, 2>(q, k, vt, o, B, H, T, Tpad, ldo, st);
-    if (nw == 4 && groups == 4) return run_attn_grp<4, 4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
-    if (nw == 8 && groups == 2) return run_attn_grp<8, 2>(q, k, vt, o, B, H, T, Tpad, ldo, st);
-    if (nw == 8 && groups == 4) return run_attn_grp<8, 4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
-  }
   if (nw != 4 && nw != 8) {
     // 256-query workgroups share each K/V^T tile over 8 waves once the grid
     // fills the chip (2 per CU); smaller grids take 128-query groups and,
@@ -591,6 +585,20 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
     split = 1;
     if (nw == 4 && g128 < 256)
       while (split < 8 && nkt >= 7 * (split + 1) && g128 * (split + 1) <= 400) ++split;
+    // a two-way split runs as two key groups of one 8-wave workgroup, merged
+    // through LDS (no fp32 partials, no combine launch): ViT-L 518^2 B=1
+    // 3.91 -> 3.74 ms per forward, same box (profiles/r03_v4_*)
+    if (nw == 4 && split == 2) {
+      nw = 8;
+      split = 1;
+      groups = 2;
+    }
+  }
+  if (groups > 1 && nkt >= groups) {
+    if (nw == 4 && groups == 2) return run_attn_grp<4, 2>(q, k, vt, o, B, H, T, Tpad, ldo, st);
+    if (nw == 4 && groups == 4) return run_attn_grp<4, 4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
+    if (nw == 8 && groups == 2) return run_attn_grp<8, 2>(q, k, vt, o, B, H, T, Tpad, ldo, st);
+    if (nw == 8 && groups == 4) return run_attn_grp<8, 4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
   }
   if (nw == 8 && qs2 && split <= 1) return run_attn<8, 2, 2>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, 1, st);
   if (nw == 4 && qs2 && split <= 1) return run_attn<4, 2, 2>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, 1, st);

@@ -166,13 +166,15 @@ bool lnfold_off() {
 }
 
 // Fork the DPT reassemble + layerN_rn work of taps 0..2 onto a side stream
-// while the encoder's remaining blocks run, when the encoder's launches leave
-// the chip under-filled: at most ~2 workgroups per CU in its widest GEMM
-// (128^2 tiles of the MLP's first linear).  MDE_DPT_FORK=0 / 1 overrides
-// (read per forward: tests toggle it; a captured graph keeps its choice).
+// while the encoder's remaining blocks run (small grids only: at most ~2
+// workgroups per CU in the encoder's widest GEMM).  Off unless MDE_DPT_FORK=1
+// (read per forward; a captured graph keeps its choice): measured slower on
+// MI355X -- ViT-L 518^2 B=1 3.66 -> 3.91 ms per forward, ViT-S B=1 0.90 ->
+// 1.11 ms (profiles/r03_v4_*): the branch's split-K convs fill the chip and
+// stretch the latency-bound encoder launches by more than they hide.
 bool dpt_fork(const mde_engine& e, int B) {
   const char* s = getenv("MDE_DPT_FORK");
-  if (s && s[0]) return s[0] == '1';
+  if (!(s && s[0] == '1')) return false;
   const long long tiles = (long long)((B * e.T + 127) / 128) * ((e.cfg.mlp_hidden + 127) / 128);
   return tiles <= 512;
 }

@@ -126,9 +126,10 @@ def test_attention(gpu, B, H, T):
 @pytest.mark.parametrize("B,H,T,spiky", [(1, 6, 1370, False), (1, 16, 1370, False), (1, 2, 700, True),
                                          (2, 6, 1370, False)])
 def test_attention_split_kv(gpu, B, H, T, spiky):
-    """Batch-1 grids split the key range (launch_attention; 4 ways at 6 x
-    1370, 2 at 16 x 1370) and merge the fp32 partials (attn_combine_kernel);
-    B=2 at 6 heads stays unsplit through the same entry point."""
+    """Batch-1 grids split the key range (launch_attention): 3 ways at 6 x
+    1370 over workgroups, merging the fp32 partials (attn_combine_kernel); 2
+    ways at 16 x 1370 as two key groups of one 8-wave workgroup, merged
+    through LDS; B=2 at 6 heads stays unsplit through the same entry point."""
     Tp = -(-T // 64) * 64
     q = rn(B * H, T, 64) * 0.125 * 2.0 * LOG2E
     k = rn(B * H, T, 64) * 2.0
