@@ -143,7 +143,7 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
   constexpr int INS = 8 / NWQ;       // glds instructions per wave per image (8 per 64-row image)
   constexpr int PER_TILE = 2 * INS;  // vmcnt entries one tile adds per wave (K + V^T)
   static_assert(NWQ * NS == NW && (NWQ == 1 || NWQ == 2 || NWQ == 4 || NWQ == 8), "waves per key group");
-  static_assert(NW == 4 || NW == 8, "waves per workgroup");
+  static_assert(NW == 4 || NW == 8 || (NS > 1 && (NW == 12 || NW == 16)), "waves per workgroup");
   static_assert(R >= 2 && R <= 4, "ring depth");
   constexpr int DIST = R - 1;  // tiles in flight ahead of the one computed
   constexpr int RING_B = R * NS * SLOT, MERGE_B = (NS - 1) * NWQ * MERGE_WAVE_B;
@@ -573,7 +573,7 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
     const char* gp = strchr(forced, 'g');  // "<waves>g<groups>": in-workgroup key groups
     if (gp) groups = atoi(gp + 1);
   }
-  if (nw != 4 && nw != 8) {
+  if (nw != 4 && nw != 8 && !(groups > 1 && (nw == 12 || nw == 16))) {
     // 256-query workgroups share each K/V^T tile over 8 waves once the grid
     // fills the chip (2 per CU); smaller grids take 128-query groups and,
     // below one group per CU, split the keys -- at least 7 key tiles per
@@ -585,10 +585,18 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
     split = 1;
     if (nw == 4 && g128 < 256)
       while (split < 8 && nkt >= 7 * (split + 1) && g128 * (split + 1) <= 400) ++split;
-    // a two-way split runs as two key groups of one 8-wave workgroup, merged
-    // through LDS (no fp32 partials, no combine launch): ViT-L 518^2 B=1
-    // 3.91 -> 3.74 ms per forward, same box (profiles/r03_v4_*)
-    if (nw == 4 && split == 2) {
+    // the split runs as key groups inside 8-wave workgroups, merged through
+    // LDS (no fp32 partials, no combine launch): two groups of 128 queries
+    // (64 KB LDS, two workgroups per CU) for a two-way split -- ViT-L 518^2
+    // B=1 3.52 -> 3.38 ms per forward --, four groups of 64 queries (128 KB,
+    // one per CU) when that grid fits the CUs -- ViT-S B=1 0.890 -> 0.859 ms
+    // (same box, profiles/r03_v5_*)
+    const long long g64 = (long long)((T + 63) / 64) * B * H;
+    if (nw == 4 && split >= 3 && g64 <= 256 && nkt >= 4) {
+      nw = 8;
+      split = 1;
+      groups = 4;
+    } else if (nw == 4 && split == 2) {
       nw = 8;
       split = 1;
       groups = 2;
@@ -599,6 +607,8 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
     if (nw == 4 && groups == 4) return run_attn_grp<4, 4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
     if (nw == 8 && groups == 2) return run_attn_grp<8, 2>(q, k, vt, o, B, H, T, Tpad, ldo, st);
     if (nw == 8 && groups == 4) return run_attn_grp<8, 4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
+    if (nw == 12 && groups == 3) return run_attn_grp<12, 3>(q, k, vt, o, B, H, T, Tpad, ldo, st);
+    if (nw == 16 && groups == 4) return run_attn_grp<16, 4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
   }
   if (nw == 8 && qs2 && split <= 1) return run_attn<8, 2, 2>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, 1, st);
   if (nw == 4 && qs2 && split <= 1) return run_attn<4, 2, 2>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, 1, st);

@@ -123,7 +123,9 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
   // counted vmcnt names "stage kt has landed"
   constexpr int SGWANT = STG > 0 ? STG : (BK == 32 ? MDE_BK32_STAGES : MDE_GEMM_STAGES);
   constexpr int SGMAX = 163840 / STAGE < SGWANT ? 163840 / STAGE : SGWANT;  // LDS limit
-  constexpr int SG = (AM == A_DENSE && AINS % NW == 0 && BINS % NW == 0 && SGMAX > 2) ? SGMAX : 2;
+  // (implicit-im2col A too: its glds count per wave is the same every stage;
+  // the register-staged upsampling A keeps the two-stage loop)
+  constexpr int SG = (AM != A_CONV3_UP && AINS % NW == 0 && BINS % NW == 0 && SGMAX > 2) ? SGMAX : 2;
   constexpr int NPER = APASS + BPASS;
   static_assert(SG >= 2 && SG <= 4, "stages");
   // folded LayerNorm consumers: (mean, var) of the tile's rows behind the ring
@@ -139,8 +141,20 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
   // (bid % 8 shares an L2), so give each XCD a contiguous run of tiles
   // (tn fastest) -- the N-tiles of one row block then share A in one L2.
   // Bijective for any grid size (cdna_hip_programming.md section 5).
-  int bid = blockIdx.x;
-  if (MDE_XCD_REMAP) bid = xcd_remap(bid, gridDim.x);
+  int bid = blockIdx.x, slice = blockIdx.y;
+  if constexpr (EM == E_PARTIAL) {
+    // split-K: remap over (slice, tile) so each XCD takes a contiguous run of
+    // one slice's tiles -- its L2 then holds that K-slice of W and of the A
+    // rows, not every slice of both (a slice-blind order streams all of W
+    // through every XCD)
+    if (MDE_XCD_REMAP) {
+      const int lin = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+      slice = lin / gridDim.x;
+      bid = lin - slice * gridDim.x;
+    }
+  } else {
+    if (MDE_XCD_REMAP) bid = xcd_remap(bid, gridDim.x);
+  }
   int tm, tn;
   tile_of(bid, (p.M + BM - 1) / BM, ntn, AM == A_DENSE ? tile_group_m(p.N, p.K, BM) : 1, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
@@ -201,7 +215,7 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
   int nk = (p.K + BK - 1) / BK, kt0 = 0;
   if constexpr (EM == E_PARTIAL) {
     const int per = (nk + (int)gridDim.y - 1) / (int)gridDim.y;
-    kt0 = (int)blockIdx.y * per;
+    kt0 = slice * per;
     nk = min(nk - kt0, per);  // >= 1: the launcher uses at most nk slices of ceil(nk / S) tiles
   }
 
@@ -501,6 +515,16 @@ int tile_override() {
   }
 }
 
+// 64^2 tiles of a grid that fits two workgroups per CU run a 4-deep ring (64
+// KB: 48 KB of K-steps in flight instead of 16): the batch-1 linears and
+// split-K slices are latency-bound on their one K-step in flight.
+// MDE_GEMM_DEEP64=0 turns it off (read per launch).
+bool deep64(long long wgs) {
+  const char* e = getenv("MDE_GEMM_DEEP64");
+  if (e && e[0] == '0') return false;
+  return wgs <= 512;
+}
+
 // 128^2 tiles once the grid holds at least this many of them (MDE_GEMM_BIG_MIN: tuning)
 long long big_tile_min() {
   static const long long v = [] {
@@ -589,6 +613,9 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
       }
       return run<128, 128, 2, 2, AM, EM>(p, st);
     }
+    if constexpr (AM == A_DENSE) {
+      if (deep64((long long)((p.M + 63) / 64) * ((p.N + 63) / 64))) return run<64, 64, 2, 2, AM, EM, 64, 4>(p, st);
+    }
     return run<64, 64, 2, 2, AM, EM>(p, st);
   }
 }
@@ -662,8 +689,12 @@ hipError_t launch_split_store(const GemmParams& p, int S, hipStream_t st) {
   q.x32 = p.partial;
   q.ldo = p.N;
   const unsigned tiles = (unsigned)(((p.M + 63) / 64) * ((p.N + 63) / 64));
-  hipLaunchKernelGGL((gemm_kernel<64, 64, MDE_GEMM_BK, 2, 2, AM, E_PARTIAL>), dim3(tiles, (unsigned)S), dim3(256), 0,
-                     st, q);
+  if (deep64((long long)tiles * S))
+    hipLaunchKernelGGL((gemm_kernel<64, 64, MDE_GEMM_BK, 2, 2, AM, E_PARTIAL, 4>), dim3(tiles, (unsigned)S), dim3(256),
+                       0, st, q);
+  else
+    hipLaunchKernelGGL((gemm_kernel<64, 64, MDE_GEMM_BK, 2, 2, AM, E_PARTIAL>), dim3(tiles, (unsigned)S), dim3(256), 0,
+                       st, q);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
   return launch_splitk_store(p.partial, S, p, st);
@@ -725,8 +756,12 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
                          dim3(256), 0, st, q);
     } else {
       const unsigned tiles = (unsigned)(((p.M + 63) / 64) * ((p.N + 63) / 64));
-      hipLaunchKernelGGL((gemm_kernel<64, 64, MDE_GEMM_BK, 2, 2, A_DENSE, E_PARTIAL>), dim3(tiles, (unsigned)S),
-                         dim3(256), 0, st, q);
+      if (deep64((long long)tiles * S))
+        hipLaunchKernelGGL((gemm_kernel<64, 64, MDE_GEMM_BK, 2, 2, A_DENSE, E_PARTIAL, 4>), dim3(tiles, (unsigned)S),
+                           dim3(256), 0, st, q);
+      else
+        hipLaunchKernelGGL((gemm_kernel<64, 64, MDE_GEMM_BK, 2, 2, A_DENSE, E_PARTIAL>), dim3(tiles, (unsigned)S),
+                           dim3(256), 0, st, q);
     }
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
