@@ -32,8 +32,13 @@
 // with v_permlane32_swap so each lane stores 16 B of one output row.
 //
 // Small grids (batch 1: 6 or 16 heads x a few query blocks) split the key
-// range over gridDim.z: each split writes its unnormalised fp32 O with its
-// running max and sum, and attn_combine_kernel merges them.
+// range.  Default: inside the workgroup -- NS key groups of NW / NS query
+// waves, each group streaming its own slice of the key tiles through its own
+// ring slots, the groups' (O, m, l) merged through LDS after the loop (ViT-L
+// B=1: 2 groups of 128 queries; ViT-S B=1: 4 groups of 64).  Fallback (grids
+// too large for that, MDE_ATTN_CFG "4s<n>"): over gridDim.z, each split
+// writing its unnormalised fp32 O with its running max and sum for
+// attn_combine_kernel to merge.
 //
 // Measured alternatives (MI355X, B = 28): two 32-query
 // sub-blocks per wave (256 VGPRs), 128-key tiles, one-block software

@@ -470,7 +470,7 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
         p, acc, [&](int row) { return m0w + row < p.M ? m0w + row : -1; }, n0 + wn * TN * 16, lane,
         smem + wave * (TM * 16) * (TN * 16) * (STG_HALF ? 2 : 4));
   }
-  if (!staged) store_tile<EM, TM, TN>(p, acc, mrow, n0 + wn * TN * 16 + (lane >> 4) * 4, lane);
+  if (!staged) store_tile<EM, TM, TN>(p, acc, mrow, n0 + wn * TN * 16 + (lane >> 4) * 4, lane, slice);
 }
 template <int BM, int BN, int WM, int WN, int AM, int EM, int BKSEL = MDE_GEMM_BK, int STG = 0>
 hipError_t run(const GemmParams& p, hipStream_t st) {
@@ -523,6 +523,17 @@ bool deep64(long long wgs) {
   const char* e = getenv("MDE_GEMM_DEEP64");
   if (e && e[0] == '0') return false;
   return wgs <= 512;
+}
+
+// 128^2 tiles of a grid under two workgroups per CU run 8 waves (2 x 4 of 64
+// x 32): a lone workgroup per CU otherwise has one wave per SIMD to cover its
+// own LDS reads and barrier waits.  ViT-L B=1 fc1 0.665 -> 0.635, fc2 (split
+// slices) 0.830 -> 0.809 ms per forward (profiles/r03_v4_bench_vitl1w8).
+// MDE_GEMM_W8SMALL=0 turns it off (read per launch).
+bool w8small(long long wgs) {
+  const char* e = getenv("MDE_GEMM_W8SMALL");
+  if (e && e[0] == '0') return false;
+  return wgs < 512;
 }
 
 // 128^2 tiles once the grid holds at least this many of them (MDE_GEMM_BIG_MIN: tuning)
@@ -610,6 +621,7 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
       // update; ViT-L B=8 qkv 2.56 -> 2.67)
       if constexpr (AM == A_DENSE && (EM == E_STORE || EM == E_QKV)) {
         if (p.K <= bk32_kmax() && bk32_tiles()) return run<128, 128, 2, 2, AM, EM, 32>(p, st);
+        if (w8small(big)) return run<128, 128, 2, 4, AM, EM>(p, st);
       }
       return run<128, 128, 2, 2, AM, EM>(p, st);
     }
@@ -748,7 +760,7 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
     if (big && tile_override() == 6 && t192 * 4 <= 256) {
       hipLaunchKernelGGL((gemm_kernel<192, 128, MDE_GEMM_BK, 2, 2, A_DENSE, E_PARTIAL, 3>),
                          dim3((unsigned)t192, (unsigned)S), dim3(256), 0, st, q);
-    } else if (big && tile_override() == 5) {
+    } else if (big && (tile_override() == 5 || w8small(t128 * S))) {
       hipLaunchKernelGGL((gemm_kernel<128, 128, MDE_GEMM_BK, 2, 4, A_DENSE, E_PARTIAL>), dim3((unsigned)t128, (unsigned)S),
                          dim3(512), 0, st, q);
     } else if (big) {

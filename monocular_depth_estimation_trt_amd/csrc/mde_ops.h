@@ -22,7 +22,7 @@ enum EMode : int {
   E_PATCH = 3,   // x32[(b*T+tok0+p)*ldo+n] = acc + bias[n] + pos[p*ldo+n]
   E_CONVT = 4,   // ConvTranspose(k=s) pixel-shuffle store into NHWC f16
   E_HEAD = 5,    // relu(acc+bias(+pe)) . w2 + b2 -> sigmoid*max | relu | exp -> fp32 map
-  E_PARTIAL = 6  // split-K slice blockIdx.y: x32[y*M*ldo + m*ldo + n] = acc (internal to the E_RESID split path)
+  E_PARTIAL = 6  // split-K slice s (blockIdx.y, XCD-remapped): x32[s*M*ldo + m*ldo + n] = acc (split paths only)
 };
 
 enum Act : int { ACT_NONE = 0, ACT_RELU = 1, ACT_GELU = 2 };

@@ -25,8 +25,10 @@ MDE_DEV void poison_ln_partials(const GemmParams& p, int row, int n) {
       make_float2(__builtin_nanf(""), __builtin_nanf(""));
 }
 
+// slice: the split-K slice of an E_PARTIAL tile (its fp32 slab in x32)
 template <int EM, int TM, int TN>
-MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&mrow)[TM], int ncol, int lane) {
+MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&mrow)[TM], int ncol, int lane,
+                        int slice = 0) {
   if constexpr (EM == E_HEAD) {
     static_assert(TN == 2, "head epilogue needs the full 32-channel row in one wave (BN 32, WN 1)");
 #pragma unroll
@@ -55,7 +57,7 @@ MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&m
     }
     return;
   } else if constexpr (EM == E_PARTIAL) {
-    float* dst = p.x32 + (size_t)blockIdx.y * p.M * p.ldo;
+    float* dst = p.x32 + (size_t)slice * p.M * p.ldo;
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int n = ncol + j * 16;
