@@ -6,8 +6,9 @@ fusion levels, the 1536^2 head and the FOV head -- with narrow layers so the
 CPU oracle runs in seconds.
 
 Tolerance (fp16 operands, fp32 accumulation vs the fp32 oracle), stated
-here: canonical inverse depth rel_mean <= 1 %, Pearson corr >= 0.999,
-per pixel |d - d_ref| <= 3 % of the map's max; FOV |deg - ref| <= 2e-2 + 1 %.
+per test at ~3x the measured error: canonical inverse depth rel_mean <=
+4e-3 (tiny) / 2e-3 (real widths), Pearson corr >= 0.99999, per pixel
+|d - d_ref| <= 0.045 / 0.05; FOV within 1e-3 deg at the real widths.
 The kernels with no arithmetic freedom (pyramid patch gather, token merge)
 are held to f16 rounding of the fp32 reference.
 """

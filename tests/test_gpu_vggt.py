@@ -6,9 +6,10 @@ frames, and "vggt_1b_shallow" -- every kernel shape of VGGT-1B at 518^2
 2 + 4 blocks so the CPU oracle finishes in seconds.
 
 Tolerance (fp16 operands, fp32 accumulation vs the fp32 oracle), stated
-here: depth rel_mean <= 1 %, Pearson corr >= 0.999, per pixel
-|d - d_ref| <= 3 % of the map's max.  The bandwidth kernels (q/k norm +
-RoPE, tap LayerNorm) are held to f16 rounding of the fp32 reference.
+per case in _check's callers at ~3x the measured error: depth rel_mean <=
+2e-3 (tiny) / 3e-3 (VGGT-1B widths), Pearson corr >= 0.99999, per pixel
+|d - d_ref| <= 0.012-0.02.  The bandwidth kernels (q/k norm + RoPE, tap
+LayerNorm) are held to f16 rounding of the fp32 reference.
 """
 
 import os
