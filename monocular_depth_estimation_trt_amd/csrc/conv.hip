@@ -645,140 +645,6 @@ upconv_kernel(const GemmParams p) {
   }
 }
 
-// ---------------------------------------------------------------------------
-// Weight-resident persistent direct conv: 3x3 / pad 1 / stride 1, 64 -> 64
-// channels, plain A (the ViT-S DPT's RCU convs and layer1_rn, F = 64).
-//
-// conv3_kernel restages the 9 weight taps (72 KB) for every 8 x 16-pixel
-// tile next to a 23 KB input patch, so 3/4 of its L2 -> LDS traffic is the
-// same weights again (B=48: 657 MB of weight fills per 148^2 launch against
-// 210 MB of patches), and that fill rate bounds it.  Here one workgroup per
-// CU keeps all 9 taps resident, walks a contiguous run of 16 x 16-pixel
-// tiles of its XCD's share, and streams only the 18 x 18 patches through a
-// two-slot ring (tile t+1's patch in flight under tile t's MFMAs).  8 waves
-// x (2 tile rows x 64 channels); the per-tile K order (tap-major, then the
-// 64 channels in two 32-deep steps) is conv3_kernel's, so the output is
-// bit-identical.  Pre-activation ReLU applies to the fragments as they are
-// read.  Epilogue: store_tile (the LDS holds weights + ring: 154 KB).
-constexpr int WTH = 16, WTW = 16;
-constexpr int WPW = WTW + 2, WPHW = (WTH + 2) * WPW;  // 18 x 18 patch
-constexpr int WPINS = (WPHW + 7) / 8;                   // glds wave-instructions per patch (8 pixels of 128 B)
-constexpr int WPATCH = WPINS * 8 * 128;
-constexpr int WWB = 9 * 64 * 128;                       // weights: (tap, out channel) rows of 64 f16
-
-__global__ void __launch_bounds__(512) conv_wres_kernel(const GemmParams p) {
-  constexpr int TM = 2, TN = 4, NW = 8;
-  __shared__ __attribute__((aligned(16))) char smem[WWB + 2 * WPATCH];
-  char* const sW = smem;
-  char* const sP0 = smem + WWB;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int Ho = p.oh, Wo = p.ow;
-  const int tiles_x = (Wo + WTW - 1) / WTW, tiles_y = (Ho + WTH - 1) / WTH;
-  const int ntiles = p.cb * tiles_x * tiles_y;
-  // XCD x (= blockIdx % 8, one L2) owns tiles [x nt / 8, (x+1) nt / 8); its
-  // workgroups stride through them, so the tiles in flight on an XCD are
-  // neighbours sharing halo rows in its L2
-  const int x8 = blockIdx.x & 7, g8 = (int)gridDim.x >> 3;
-  int t = (int)((long long)x8 * ntiles / 8) + (int)(blockIdx.x >> 3);
-  const int tend = (int)((long long)(x8 + 1) * ntiles / 8);
-  if (t >= tend) return;  // uniform, before any load is issued
-
-  const int lrow = lane >> 3;
-  const int lch = cpch<64>(lrow, lane & 7);  // logical chunk this lane fetches (glds)
-  // weights: 72 glds wave-instructions of 8 rows (9 per wave), row r of tap
-  // tp at LDS row tp * 64 + r
-  for (int q = wave; q < 72; q += NW) {
-    const int tp = q >> 3, r = (q & 7) * 8 + lrow;
-    glds16c(reinterpret_cast<const f16*>(p.W) + (size_t)r * p.ldw + tp * 64 + lch * 8, sW + q * 8 * 128);
-  }
-  auto load_patch = [&](int tt, char* sP) {
-    const int tx = tt % tiles_x, r = tt / tiles_x;
-    const int ty = r % tiles_y, b = r / tiles_y;
-    const int iy0 = ty * WTH - 1, ix0 = tx * WTW - 1;
-    const f16* img = reinterpret_cast<const f16*>(p.A) + (size_t)b * p.ch * p.cw * 64;
-    for (int q = wave; q < WPINS; q += NW) {
-      const int pp = q * 8 + lrow;
-      const int py = pp / WPW, px = pp - (pp / WPW) * WPW;
-      const int iy = iy0 + py, ix = ix0 + px;
-      const bool ok = pp < WPHW && iy >= 0 && iy < p.ch && ix >= 0 && ix < p.cw;
-      const f16* src = ok ? img + ((size_t)iy * p.cw + ix) * 64 + lch * 8 : g_zero_conv;
-      glds16c(src, sP + q * 8 * 128);
-    }
-  };
-
-  f32x4 acc[TM][TN];
-#pragma unroll
-  for (int i = 0; i < TM; ++i)
-#pragma unroll
-    for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-
-  int cur = 0;
-  load_patch(t, sP0);
-  for (;;) {
-    wait_vmc();       // tile t's patch (and, the first time, the weights) landed
-    __syncthreads();  // ... for every wave; every wave is done with the other ring slot
-    const int tn = t + g8;
-    if (tn < tend) load_patch(tn, sP0 + (cur ^ 1) * WPATCH);
-    const char* sP = sP0 + cur * WPATCH;
-#pragma unroll
-    for (int tp = 0; tp < 9; ++tp) {
-      const int ky = tp / 3, kx = tp - (tp / 3) * 3;
-#pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        const int lc = 4 * s + (lane >> 4);
-        f16x8 fa[TM], fb[TN];
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int pp = (wave * TM + i + ky) * WPW + (lane & 15) + kx;
-          fa[i] = *reinterpret_cast<const f16x8*>(sP + pp * 128 + cpch<64>(pp, lc) * 16);
-          if (p.relu_in) fa[i] = relu8(fa[i]);
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int r = tp * 64 + j * 16 + (lane & 15);
-          fb[j] = *reinterpret_cast<const f16x8*>(sW + r * 128 + cpch<64>(r, lc) * 16);
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);
-      }
-    }
-    {
-      const int tx = t % tiles_x, r = t / tiles_x;
-      const int ty = r % tiles_y, b = r / tiles_y;
-      int mrow[TM];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int oy = ty * WTH + wave * TM + i, ox = tx * WTW + (lane & 15);
-        mrow[i] = (oy < Ho && ox < Wo) ? ((b * Ho + oy) * Wo + ox) : -1;
-      }
-      store_tile<E_STORE, TM, TN>(p, acc, mrow, (lane >> 4) * 4, lane);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-    if (tn >= tend) break;
-    t = tn;
-    cur ^= 1;
-  }
-}
-
-// conv_wres_kernel takes a launch when: plain A, stride 1, 64 -> 64 channels,
-// E_STORE, and a grid of at least one 16 x 16 tile per CU.  MDE_CONV_WRES=0
-// keeps conv3_kernel (read per call: tests compare both).
-bool conv_wres_eligible(const GemmParams& p) {
-  const char* e = getenv("MDE_CONV_WRES");
-  if (e && e[0] == '0') return false;
-  if (p.amode != A_CONV3 || p.emode != E_STORE || p.stride != 1 || p.cc != 64 || p.N != 64) return false;
-  if (p.ldw < 9 * 64 || (p.ldo & 3)) return false;
-  const long long tiles = (long long)p.cb * ((p.oh + WTH - 1) / WTH) * ((p.ow + WTW - 1) / WTW);
-  return tiles >= 256;
-}
-
 // MDE_UPCONV=0: the upsampling convs stay on conv3_kernel (A/B; read per
 // call so a test can compare both kernels -- captured graphs keep their choice)
 bool upconv_enabled() {
@@ -855,10 +721,6 @@ hipError_t launch_conv3(const GemmParams& p, hipStream_t st) {
   if (p.emode != E_STORE) return hipErrorInvalidValue;
   if (up) return ck64 ? conv_tiles<64, 1, true, E_STORE>(p, st) : conv_tiles<32, 1, true, E_STORE>(p, st);
   if (p.stride == 2) return conv_tiles<32, 2, false, E_STORE>(p, st);
-  if (conv_wres_eligible(p)) {
-    hipLaunchKernelGGL(conv_wres_kernel, dim3(256), dim3(512), 0, st, p);  // one per CU (154 KB LDS)
-    return hipGetLastError();
-  }
   return ck64 ? conv_tiles<64, 1, false, E_STORE>(p, st) : conv_tiles<32, 1, false, E_STORE>(p, st);
 }
 

@@ -126,10 +126,11 @@ def test_attention(gpu, B, H, T):
 @pytest.mark.parametrize("B,H,T,spiky", [(1, 6, 1370, False), (1, 16, 1370, False), (1, 2, 700, True),
                                          (2, 6, 1370, False)])
 def test_attention_split_kv(gpu, B, H, T, spiky):
-    """Batch-1 grids split the key range (launch_attention): 3 ways at 6 x
-    1370 over workgroups, merging the fp32 partials (attn_combine_kernel); 2
-    ways at 16 x 1370 as two key groups of one 8-wave workgroup, merged
-    through LDS; B=2 at 6 heads stays unsplit through the same entry point."""
+    """Small grids split the key range (launch_attention's policy): B=1 at 6
+    x 1370 as four key groups of 64 queries in one 8-wave workgroup, at 16 x
+    1370 as two groups of 128 (merged through LDS); B=2 at 6 x 1370 (264
+    64-query groups: more than the CUs) over workgroups, merging the fp32
+    partials (attn_combine_kernel); 2 x 700 unsplit (too few key tiles)."""
     Tp = -(-T // 64) * 64
     q = rn(B * H, T, 64) * 0.125 * 2.0 * LOG2E
     k = rn(B * H, T, 64) * 2.0
@@ -270,41 +271,6 @@ def test_conv3x3(gpu, B, h, w, cin, cout, stride, relu_in, act, nres):
     op("mde_op_conv3x3", ptr(nhwc(x).half().to(gpu)), B, h, w, cin, ptr(wp), wp.shape[1], cout, stride, relu_in,
        ptr(b.to(gpu)), act, ptr(rg[0]), ptr(rg[1]), ptr(out), stream())
     close(nchw(out), ref, 1e-2, 1e-2, f"conv3x3 {h}x{w} {cin}->{cout} s{stride}")
-
-
-@pytest.mark.parametrize("B,h,w,relu_in,act,nres", [(3, 148, 148, 1, 1, 2), (32, 37, 37, 1, 0, 1),
-                                                     (20, 75, 41, 0, 0, 0), (4, 149, 131, 1, 1, 1)])
-def test_conv_weight_resident(gpu, B, h, w, relu_in, act, nres):
-    """64 -> 64 convs on grids of >= 256 16x16 tiles take the weight-resident
-    persistent kernel (conv.hip conv_wres_kernel): against torch, and bit for
-    bit against conv3_kernel (MDE_CONV_WRES=0) -- same per-tile K order;
-    ragged maps (149 x 131: partial tiles in both directions)."""
-    import os
-    cin = cout = 64
-    x = rn(B, cin, h, w)
-    wt, b = rn(cout, cin, 3, 3, scale=(9 * cin) ** -0.5), rn(cout, scale=0.02)
-    xin = x.half().float()
-    ref = F.conv2d(F.relu(xin) if relu_in else xin, wt.half().float(), b, padding=1)
-    if act == 1:
-        ref = F.relu(ref)
-    res = [rn(*ref.shape) for _ in range(nres)]
-    for r in res:
-        ref = ref + r.half().float()
-    wp = conv_w(wt).to(gpu)
-    rg = [nhwc(r).half().to(gpu) for r in res] + [None, None]
-    xg, bg = nhwc(x).half().to(gpu), b.to(gpu)
-    got = []
-    for flag in ("1", "0"):
-        os.environ["MDE_CONV_WRES"] = flag
-        try:
-            out = torch.empty(B, h, w, cout, dtype=torch.float16, device=gpu)
-            op("mde_op_conv3x3", ptr(xg), B, h, w, cin, ptr(wp), wp.shape[1], cout, 1, relu_in, ptr(bg), act,
-               ptr(rg[0]), ptr(rg[1]), ptr(out), stream())
-        finally:
-            os.environ.pop("MDE_CONV_WRES", None)
-        got.append(out)
-    close(nchw(got[0]), ref, 1e-2, 1e-2, f"conv weight-resident {B}x{h}x{w}")
-    assert torch.equal(got[0], got[1]), "weight-resident conv must equal conv3_kernel bit for bit"
 
 
 # E_STORE split-K (launch_gemm's small-grid policy): the batch-1 ViT-L DPT
