@@ -685,7 +685,10 @@ int store_split_slices(const GemmParams& p) {
     return e ? atoi(e) : 12;
   }();
   if (wgs >= 256 || nk < nkmin) return 1;
+  // fill two workgroups per CU without spilling into a third: the slices then
+  // run the 4-deep ring (deep64), which a 513th workgroup would forfeit
   int S = (int)((512 + t64 - 1) / t64);
+  if (deep64(1) && 512 / t64 >= 2) S = (int)(512 / t64);
   S = S < nk / 4 ? S : nk / 4;  // >= 4 K-steps per slice
   S = S < 16 ? S : 16;
   while (S > 1 && (size_t)S * p.M * p.N > p.partial_cap) --S;
@@ -747,6 +750,10 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
     const char* e128 = getenv("MDE_SPLITK128");
     const bool big = t128 * 4 >= 320 && nk >= 16 && !(e128 && e128[0] == '0');
     int S = big ? 4 : (p.splitk < nk ? p.splitk : nk);
+    if (!big && deep64(1)) {  // keep the 64^2 slices within two workgroups per CU (deep ring)
+      const long long t64 = (long long)((p.M + 63) / 64) * ((p.N + 63) / 64);
+      while (S > 2 && t64 * S > 512) --S;
+    }
     const int per = (nk + S - 1) / S;
     S = (nk + per - 1) / per;  // every slice non-empty
     GemmParams q = p;
