@@ -462,44 +462,52 @@ upconv_kernel(const GemmParams p) {
     return g;
   };
 
+  // Both passes map a thread to a fixed (patch column, 8-channel chunk) --
+  // CL = 72 pairs -- and one of RG = 7 row groups (504 of the 512 threads),
+  // stepping over rows: the column's source index, weight and bounds are
+  // computed once per tile, not per item.
+  constexpr int CL = UPW * 4, RG = NT / CL;
+  static_assert(RG * 2 >= USR && RG * 3 >= UPH, "row groups cover the H rows (2 each) and the patch rows (3)");
   // ---- pass H operands of item (tile g, chunk c): HI (source row, patch
-  // column, 8-channel chunk) items per thread, both source columns loaded
-  // into registers -- issued one item ahead, under the previous item's
-  // pass V, MFMAs and epilogue
-  constexpr int HI = (USR * UPW * 4 + NT - 1) / NT;
+  // column, chunk) items per thread, both source columns loaded into
+  // registers -- issued one item ahead, under the previous item's pass V,
+  // MFMAs and epilogue
+  constexpr int HI = 2;
   f16x8 ha[HI], hb[HI];
-  f16 hw[HI];
-  bool hs[HI], hin[HI];
+  f16 hw = (f16)0.0f;
+  bool hs[HI], hin = false;
   auto h_issue = [&](const Geo& g, int c, int tid) {
     const f16* img = reinterpret_cast<const f16*>(p.A) + (size_t)g.b * p.ch * p.cw * p.cc;
+    const int cl = tid % CL, rg = tid / CL;
+    const int lc = cl & 3, col = cl >> 2;
+    const int ix = g.ix0 + col;
+    hin = rg < RG && ix >= 0 && ix < p.uw;
+    int x0 = 0, x1 = 0;
+    float lx0, lx1 = 0.f;
+    if (hin) ac_index(usx, ix, p.cw, x0, x1, lx0, lx1);
+    hw = (f16)lx1;
+    const unsigned o0 = (unsigned)x0 * (unsigned)p.cc + (unsigned)(c * 32 + lc * 8);
+    const unsigned o1 = (unsigned)x1 * (unsigned)p.cc + (unsigned)(c * 32 + lc * 8);
 #pragma unroll
     for (int k = 0; k < HI; ++k) {
-      const int it = tid + k * NT;
-      const int lc = it & 3, rest = it >> 2;
-      const int sr = rest / UPW, col = rest - (rest / UPW) * UPW;
-      const int ix = g.ix0 + col;
-      hs[k] = it < g.nsr * UPW * 4;
-      const bool in = hs[k] && ix >= 0 && ix < p.uw;
-      hin[k] = in;
-      int x0 = 0, x1 = 0;
-      float lx0, lx1 = 0.f;
-      if (in) ac_index(usx, ix, p.cw, x0, x1, lx0, lx1);
-      hw[k] = (f16)lx1;
-      const unsigned r = (unsigned)(g.sy0 + (in ? sr : 0)) * rowstride + (unsigned)(c * 32 + lc * 8);
+      const int sr = rg + k * RG;
+      hs[k] = rg < RG && sr < g.nsr;
+      const unsigned r = (unsigned)(g.sy0 + (hin && hs[k] ? sr : 0)) * rowstride;
       // (out-of-map columns load a valid pixel and are zeroed at the commit:
       // a select here would wait for the load)
-      ha[k] = *reinterpret_cast<const f16x8*>(img + (r + (unsigned)x0 * (unsigned)p.cc));
-      hb[k] = *reinterpret_cast<const f16x8*>(img + (r + (unsigned)x1 * (unsigned)p.cc));
+      ha[k] = *reinterpret_cast<const f16x8*>(img + (r + o0));
+      hb[k] = *reinterpret_cast<const f16x8*>(img + (r + o1));
     }
   };
   auto h_commit = [&](int tid) {
+    const int cl = tid % CL, rg = tid / CL;
+    const int lc = cl & 3, col = cl >> 2;
 #pragma unroll
     for (int k = 0; k < HI; ++k) {
-      const int it = tid + k * NT;
       if (hs[k]) {
-        const int lc = it & 3, hp = it >> 2;  // hp = sr * UPW + col
+        const int hp = (rg + k * RG) * UPW + col;
         *reinterpret_cast<f16x8*>(sH + hp * 64 + cpch<32>(hp, lc) * 16) =
-            hin[k] ? lerp8(ha[k], hb[k], hw[k]) : zero8();
+            hin ? lerp8(ha[k], hb[k], hw) : zero8();
       }
     }
   };
@@ -534,25 +542,30 @@ upconv_kernel(const GemmParams p) {
       gn = geo(tn);
       h_issue(gn, cn, vt);
     }
-    // ---- pass V: (patch pixel, chunk) items (not unrolled: the next item's
-    // pass-H registers are live here)
+    // ---- pass V: the thread's (column, chunk) over rows rg, rg + RG, ...
+    // (not unrolled: the next item's pass-H registers are live here)
+    {
+      const int cl = vt % CL, rg = vt / CL;
+      const int lc = cl & 3, col = cl >> 2;
+      const int ix = g.ix0 + col;
+      const bool xin = ix >= 0 && ix < p.uw;
 #pragma unroll 1
-    for (int it = vt; it < UPH * UPW * 4; it += NT) {
-      const int lc = it & 3, pp = it >> 2;
-      const int r = pp / UPW, col = pp - (pp / UPW) * UPW;
-      const int iy = g.iy0 + r, ix = g.ix0 + col;
-      f16x8 v = zero8();
-      if (iy >= 0 && iy < p.uh && ix >= 0 && ix < p.uw) {
-        int y0, y1;
-        float ly0, ly1;
-        ac_index(usy, iy, p.ch, y0, y1, ly0, ly1);
-        const int h0 = (y0 - g.sy0) * UPW + col, h1 = (y1 - g.sy0) * UPW + col;
-        const f16x8 a = *reinterpret_cast<const f16x8*>(sH + h0 * 64 + cpch<32>(h0, lc) * 16);
-        const f16x8 bb = *reinterpret_cast<const f16x8*>(sH + h1 * 64 + cpch<32>(h1, lc) * 16);
-        v = lerp8(a, bb, (f16)ly1);
-        if (p.relu_in) v = relu8(v);
+      for (int r = rg; r < UPH && rg < RG; r += RG) {
+        const int iy = g.iy0 + r;
+        f16x8 v = zero8();
+        if (xin && iy >= 0 && iy < p.uh) {
+          int y0, y1;
+          float ly0, ly1;
+          ac_index(usy, iy, p.ch, y0, y1, ly0, ly1);
+          const int h0 = (y0 - g.sy0) * UPW + col, h1 = (y1 - g.sy0) * UPW + col;
+          const f16x8 a = *reinterpret_cast<const f16x8*>(sH + h0 * 64 + cpch<32>(h0, lc) * 16);
+          const f16x8 bb = *reinterpret_cast<const f16x8*>(sH + h1 * 64 + cpch<32>(h1, lc) * 16);
+          v = lerp8(a, bb, (f16)ly1);
+          if (p.relu_in) v = relu8(v);
+        }
+        const int pp = r * UPW + col;
+        *reinterpret_cast<f16x8*>(sP + pp * 64 + cpch<32>(pp, lc) * 16) = v;
       }
-      *reinterpret_cast<f16x8*>(sP + pp * 64 + cpch<32>(pp, lc) * 16) = v;
     }
     __syncthreads();
     // ---- 9 taps x one 32-deep k-step of chunk c

@@ -78,10 +78,17 @@ VARIANTS = {
             const f16x8 c = *reinterpret_cast<const f16x8*>(img + (r1 + o0 + lc * 8));
             const f16x8 d = *reinterpret_cast<const f16x8*>(img + (r1 + o1 + lc * 8));""", "", 1),
         ("v = lerp8(lerp8(a, bq, (f16)lx1), lerp8(c, d, (f16)lx1), (f16)ly1);", "v = a;", 1)]),
-    # direct conv: no MFMAs (fragments kept live)
+    # direct conv (conv3_kernel and upconv_kernel): no MFMAs (fragments kept live)
     "conv_nomfma": ("conv.hip", [
         ("for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);",
-         'for (int j = 0; j < TN; ++j) asm volatile("" :: "v"(fb[j]), "v"(fa[i]));', 2)]),
+         'for (int j = 0; j < TN; ++j) asm volatile("" :: "v"(fb[j]), "v"(fa[i]));', 3)]),
+    # separable upsampling conv: pass V without its vertical lerp (one H row read)
+    "upconv_nov": ("conv.hip", [
+        ("          v = lerp8(a, bb, (f16)ly1);\n", "          v = a;\n          asm volatile(\"\" :: \"v\"(bb));\n", 1)]),
+    # separable upsampling conv: pass H without its horizontal lerp (loads kept)
+    "upconv_noh": ("conv.hip", [
+        ("hin ? lerp8(ha[k], hb[k], hw) : zero8();",
+         "hin ? ha[k] : hb[k];", 1)]),
     # direct conv: weights never loaded (LDS garbage)
     "conv_now": ("conv.hip", [
         ("for (int q = wave; q < BINS; q += NW) glds16c(", "for (int q = wave; q < 0; q += NW) glds16c(", 1)]),
