@@ -3,7 +3,7 @@
 # baseline), its rocprof stats + FETCH/WRITE passes, config 3's unit (ViT-L
 # B=1) bench + profile, Depth Pro and VGGT bench lines
 set -o pipefail
-O=gpurun_out/r3ev
+O=${1:-gpurun_out/r3ev}
 bash tools/gpu_tasks.sh $O tests smoke \
   bench:def: \
   profile:def \
