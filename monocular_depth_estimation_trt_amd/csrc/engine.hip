@@ -314,8 +314,29 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
   const h16* lay[4] = {b.l1, b.l2, b.pj[2], b.l4};
   const int cin[4] = {e.c1p, oc[1], oc[2], oc[3]};
   char nm[64];
+  // the taps' final LayerNorm folded into the projects (packs with proj*.wf):
+  // each project runs right after its tap block, on the raw f16 residual rows
+  // (cls rows skipped by the GEMM's row map) and that block's LN partials --
+  // before the next block rewrites both -- with W * gamma, as qkv / fc1 do
+  const bool fold_taps = fold && e.get("proj0.wf") != nullptr;
+  auto project_folded = [&](int i) {
+    const std::string pn = "proj" + std::to_string(i);
+    GemmParams g = dense(b.Xh, D, pn + ".wf", B * np, oc[i], D);
+    g.emode = E_STORE;
+    g.bias = w32(pn + ".c2");
+    g.out16 = b.pj[i];
+    g.ldo = oc[i];
+    g.lnst_in = b.st;
+    g.lnc1 = w32(pn + ".c1");
+    g.lnst_ns = D / 32;
+    g.lnst_rows = B * T;
+    g.ln_eps = cf.ln_eps;
+    g.a_tok = T;
+    snprintf(nm, sizeof nm, "reassemble%d.project", i);
+    gemm(nm, g);
+  };
   auto reassemble = [&](int i) {
-    {
+    if (!fold_taps) {
       GemmParams g = dense(b.tap[i], D, "proj" + std::to_string(i) + ".w", B * np, oc[i], D);
       g.emode = E_STORE;
       g.bias = w32("proj" + std::to_string(i) + ".b");
@@ -481,11 +502,15 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
       gemm(nm, g);
     }
     if (tap < 4 && cf.taps[tap] == i) {
-      snprintf(nm, sizeof nm, "tap%d.norm", tap);
-      h16* dst = b.tap[tap];
-      step(nm, [&] {
-        return launch_layernorm(b.X, dst, w32("norm.g"), w32("norm.b"), B * T, D, cf.ln_eps, T, 1, st, b.Xh);
-      });
+      if (fold_taps) {
+        project_folded(tap);
+      } else {
+        snprintf(nm, sizeof nm, "tap%d.norm", tap);
+        h16* dst = b.tap[tap];
+        step(nm, [&] {
+          return launch_layernorm(b.X, dst, w32("norm.g"), w32("norm.b"), B * T, D, cf.ln_eps, T, 1, st, b.Xh);
+        });
+      }
       if (fork && tap < 3) fork_reassemble(tap);
       ++tap;
     }

@@ -175,7 +175,8 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
       rv[i] = gm < p.M;
       const int gmc = rv[i] ? gm : (p.M - 1);
       if constexpr (AM == A_DENSE) {
-        arow[i] = reinterpret_cast<const f16*>(p.A) + (size_t)gmc * p.lda;
+        const int ar = p.a_tok > 1 ? gmc + gmc / (p.a_tok - 1) + 1 : gmc;
+        arow[i] = reinterpret_cast<const f16*>(p.A) + (size_t)ar * p.lda;
         iy0[i] = ix0[i] = 0;
       } else {
         const int hw = p.oh * p.ow;
@@ -363,7 +364,8 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
 #pragma unroll
         for (int g = 0; g < G; ++g) {
           const int m = m0 + wave * RPW + g * 16 + (lane & 15);
-          const int mc = m < p.M ? m : p.M - 1;
+          const int mr = m < p.M ? m : p.M - 1;
+          const int mc = p.a_tok > 1 ? mr + mr / (p.a_tok - 1) + 1 : mr;
 #pragma unroll
           for (int k = 0; k < 8; ++k) {
             const int sl = (lane >> 4) + (k < kp ? 4 * k : 0);
@@ -724,6 +726,8 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
   if (p.K <= 0 || (p.K & 7) || (p.N & 7) || (p.ldw & 63) || p.ldw < ((p.K + 63) / 64) * 64)
     return hipErrorInvalidValue;
   if (p.amode == A_DENSE && ((p.lda & 7) || p.lda < p.K)) return hipErrorInvalidValue;
+  if (p.a_tok == 1 || p.a_tok < 0 || (p.a_tok > 1 && (p.amode != A_DENSE || p.emode != E_STORE || !p.lnst_in)))
+    return hipErrorInvalidValue;
   if (p.amode != A_DENSE && (p.cc & 7)) return hipErrorInvalidValue;
   if ((p.emode == E_STORE || p.emode == E_RESID || p.emode == E_PATCH) && (p.ldo & 7)) return hipErrorInvalidValue;
   // E_CONVT stores 16 B per output pixel (f16x8 at pixel*ldo + co): ldo and
@@ -792,7 +796,9 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
     // a tile that falls back to the direct epilogue writes NaN partials)
     if (p.lnst_out && !MDE_EPI_LDS) return hipErrorInvalidValue;
     if ((p.lnst_ns * 32 != (p.lnst_out ? p.N : p.K)) ||
-        (p.lnst_in && (p.lnst_ns > 32 || (p.lnst_ns & 3) || p.lnst_rows != p.M)) ||
+        (p.lnst_in && (p.lnst_ns > 32 || (p.lnst_ns & 3) ||
+                       p.lnst_rows != (p.a_tok > 1 ? p.M / (p.a_tok - 1) * p.a_tok : p.M) ||
+                       (p.a_tok > 1 && p.M % (p.a_tok - 1)))) ||
         (p.lnst_out && p.lnst_rows < (p.emode == E_PATCH ? p.M / p.npatch * p.T : p.M)) || (p.lnst_in && (!p.lnc1 || p.amode != A_DENSE)) ||
         (p.lnst_out && !p.xh))
       return hipErrorInvalidValue;

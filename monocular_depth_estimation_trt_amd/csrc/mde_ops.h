@@ -83,6 +83,11 @@ struct GemmParams {
   float* lnst_out = nullptr;
   const float* lnst_in = nullptr; const float* lnc1 = nullptr;
   int lnst_ns = 0, lnst_rows = 0; float ln_eps = 1e-6f;
+  // A_DENSE row skip (the DPT projects reading the residual stream through
+  // the tap LayerNorm fold): a_tok > 1 -> GEMM row m reads A row (and LN
+  // partial row) (m / (a_tok - 1)) * a_tok + 1 + m % (a_tok - 1), i.e. every
+  // sequence's first (cls) row is skipped
+  int a_tok = 0;
 };
 
 // x32[m*ldo+n] += ls[n] * (sum_{s<S} P[s][m][n] + bias[n]), slices summed in

@@ -125,8 +125,9 @@ def _slice_partials(v: np.ndarray) -> np.ndarray:
 def packed_tensors(sd: Dict[str, np.ndarray], cfg: dict, img_h: int, img_w: int,
                    fold_ln: bool = False) -> "OrderedDict[str, np.ndarray]":
     """The packed tensors (name -> f16/f32 numpy array) for one input size.
-    fold_ln (precision "fp16" engines) adds the LayerNorm-folded qkv / fc1
-    weights (`*.wf`, `*.c1`, `*.c2`) and the cls row's partials (`pos.cls.st`)."""
+    fold_ln (precision "fp16" engines) adds the LayerNorm-folded qkv / fc1 /
+    DPT project weights (`*.wf`, `*.c1`, `*.c2`) and the cls row's partials
+    (`pos.cls.st`)."""
     sd = normalize_keys(sd)
     missing = [k for k in W.expected_keys(cfg) if k not in sd and not k.endswith("mask_token")]
     if missing:
@@ -178,6 +179,10 @@ def packed_tensors(sd: Dict[str, np.ndarray], cfg: dict, img_h: int, img_w: int,
         w = sd[f"{h}projects.{i}.weight"]
         o[f"proj{i}.w"] = _pad2(w.reshape(w.shape[0], w.shape[1]))
         o[f"proj{i}.b"] = f32(sd[f"{h}projects.{i}.bias"])
+        if fold_ln:  # the taps' final LayerNorm folded into the projects (engine.hip)
+            o[f"proj{i}.wf"], o[f"proj{i}.c1"], o[f"proj{i}.c2"] = _fold_ln(
+                w.reshape(w.shape[0], w.shape[1]), sd[f"{h}projects.{i}.bias"], sd[p + "norm.weight"],
+                sd[p + "norm.bias"])
     o["rs0.w"] = _convT(sd[h + "resize_layers.0.weight"])
     o["rs0.b"] = f32(sd[h + "resize_layers.0.bias"])
     o["rs1.w"] = _convT(sd[h + "resize_layers.1.weight"])
