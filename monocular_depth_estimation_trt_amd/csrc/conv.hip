@@ -354,7 +354,14 @@ hipError_t conv_tiles(const GemmParams& p, hipStream_t st) {
     return run_conv<32, 4, 1, CK, S, UP, EM>(p, st);
   } else {
     if (p.N <= 32) return run_conv<32, 4, 1, CK, S, UP, EM>(p, st);
-    if (p.N <= 64) return run_conv<64, 4, 1, CK, S, UP, EM>(p, st);
+    if (p.N <= 64) {
+      // 64-channel convs on a grid under one workgroup per CU (batch 1: the
+      // ViT-S RCUs at 148^2 are 190 tiles) split the channels over two
+      // 32-wide workgroups
+      const long long wg64 = (long long)p.cb * ((p.oh + TH - 1) / TH) * ((p.ow + TW - 1) / TW);
+      if (!UP && p.N == 64 && conv_bn64_small(0) && wg64 < 256) return run_conv<32, 4, 1, CK, S, UP, EM>(p, st);
+      return run_conv<64, 4, 1, CK, S, UP, EM>(p, st);
+    }
     const long long wg128 = (long long)p.cb * ((p.oh + TH - 1) / TH) * ((p.ow + TW - 1) / TW) * ((p.N + 127) / 128);
     if (!UP && conv_bn64_small(wg128)) return run_conv<64, 4, 1, CK, S, UP, EM>(p, st);
     return run_conv<128, 2, 2, CK, S, UP, EM>(p, st);

@@ -526,6 +526,13 @@ bool deep64(long long wgs) {
   if (e && e[0] == '0') return false;
   return wgs <= 512;
 }
+// ... and grids of up to three workgroups per CU a 3-deep ring (48 KB: two
+// K-steps in flight), e.g. ViT-S B=1 fc1 (528 64^2 tiles)
+bool deep64_3(long long wgs) {
+  const char* e = getenv("MDE_GEMM_DEEP64");
+  if (e && e[0] == '0') return false;
+  return wgs > 512 && wgs <= 768;
+}
 
 // 128^2 tiles of a grid under two workgroups per CU run 8 waves (2 x 4 of 64
 // x 32): a lone workgroup per CU otherwise has one wave per SIMD to cover its
@@ -628,7 +635,9 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
       return run<128, 128, 2, 2, AM, EM>(p, st);
     }
     if constexpr (AM == A_DENSE) {
-      if (deep64((long long)((p.M + 63) / 64) * ((p.N + 63) / 64))) return run<64, 64, 2, 2, AM, EM, 64, 4>(p, st);
+      const long long t64 = (long long)((p.M + 63) / 64) * ((p.N + 63) / 64);
+      if (deep64(t64)) return run<64, 64, 2, 2, AM, EM, 64, 4>(p, st);
+      if (deep64_3(t64)) return run<64, 64, 2, 2, AM, EM, 64, 3>(p, st);
     }
     return run<64, 64, 2, 2, AM, EM>(p, st);
   }
