@@ -526,13 +526,6 @@ bool deep64(long long wgs) {
   if (e && e[0] == '0') return false;
   return wgs <= 512;
 }
-// ... and grids of up to three workgroups per CU a 3-deep ring (48 KB: two
-// K-steps in flight), e.g. ViT-S B=1 fc1 (528 64^2 tiles)
-bool deep64_3(long long wgs) {
-  const char* e = getenv("MDE_GEMM_DEEP64");
-  if (e && e[0] == '0') return false;
-  return wgs > 512 && wgs <= 768;
-}
 
 // 128^2 tiles of a grid under two workgroups per CU run 8 waves (2 x 4 of 64
 // x 32): a lone workgroup per CU otherwise has one wave per SIMD to cover its
@@ -637,7 +630,8 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
     if constexpr (AM == A_DENSE) {
       const long long t64 = (long long)((p.M + 63) / 64) * ((p.N + 63) / 64);
       if (deep64(t64)) return run<64, 64, 2, 2, AM, EM, 64, 4>(p, st);
-      if (deep64_3(t64)) return run<64, 64, 2, 2, AM, EM, 64, 3>(p, st);
+      // (a 3-deep ring for grids of 512-768 tiles measured no gain: ViT-S B=1
+      // fc1, 528 tiles, 0.134 -> 0.136 ms per forward, profiles/r03_v11_*)
     }
     return run<64, 64, 2, 2, AM, EM>(p, st);
   }
