@@ -51,10 +51,9 @@ VARIANTS = {
     # candidate (not an ablation): static priority for the second-dispatched
     # half of an 8-wave workgroup (MI355X_MICROARCH.md "Two waves per SIMD" 4)
     "attn_prio": ("attention.hip", [
-        ("""  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // XCD-aware block order""", """  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
-  // XCD-aware block order""", 1)]),
+        ("""  const int wave = wave_all - grp * NWQ;         // query wave within the group""",
+         """  const int wave = wave_all - grp * NWQ;         // query wave within the group
+  if (NW == 8 && NS == 1 && wave_all >= 4) __builtin_amdgcn_s_setprio(1);""", 1)]),
     # GEMM main loop only: the epilogue returns unless a NaN appears (r02's
     # MDE_EXP_NOEPI, profiles/r02_v10_epilogue_cost_*)
     "gemm_noepi": ("gemm.hip", [
