@@ -337,15 +337,15 @@ hipError_t run_conv(const GemmParams& p, hipStream_t st) {
   return hipGetLastError();
 }
 
-// Wide convs (N > 64) whose 128-channel grid leaves CUs with one or two
-// workgroups (under 512: batch 1, e.g. ViT-L's 148^2 256-channel RCUs at 380)
-// take 64-channel tiles: twice the workgroups at 40 KB LDS each, so the
-// busiest CU carries ~3 half-width tiles instead of 2 full ones.
-// MDE_CONV_BN64=0 turns it off (read per call).
-bool conv_bn64_small(long long wg128) {
-  const char* e = getenv("MDE_CONV_BN64");
-  if (e && e[0] == '0') return false;
-  return wg128 < 512;
+// Narrower channel tiles for small grids (MDE_CONV_NARROW=0 turns them off,
+// read per call): wide convs (N > 64) whose 128-channel grid leaves CUs with
+// one or two workgroups (under 512: batch 1, e.g. ViT-L's 148^2 256-channel
+// RCUs at 380) take 64-channel tiles -- twice the workgroups at 40 KB LDS
+// each, the busiest CU carrying ~3 half-width tiles instead of 2 full ones;
+// 64-channel convs under one workgroup per CU take 32-channel tiles.
+bool conv_narrow_tiles() {
+  const char* e = getenv("MDE_CONV_NARROW");
+  return !(e && e[0] == '0');
 }
 
 template <int CK, int S, bool UP, int EM>
@@ -360,11 +360,11 @@ hipError_t conv_tiles(const GemmParams& p, hipStream_t st) {
       // 32-wide workgroups: ViT-S B=1 rcu.conv 0.165 -> 0.144 ms, forward
       // 0.854 -> 0.826 ms (same box, profiles/r03_v11_*)
       const long long wg64 = (long long)p.cb * ((p.oh + TH - 1) / TH) * ((p.ow + TW - 1) / TW);
-      if (!UP && p.N == 64 && conv_bn64_small(0) && wg64 < 256) return run_conv<32, 4, 1, CK, S, UP, EM>(p, st);
+      if (!UP && p.N == 64 && conv_narrow_tiles() && wg64 < 256) return run_conv<32, 4, 1, CK, S, UP, EM>(p, st);
       return run_conv<64, 4, 1, CK, S, UP, EM>(p, st);
     }
     const long long wg128 = (long long)p.cb * ((p.oh + TH - 1) / TH) * ((p.ow + TW - 1) / TW) * ((p.N + 127) / 128);
-    if (!UP && conv_bn64_small(wg128)) return run_conv<64, 4, 1, CK, S, UP, EM>(p, st);
+    if (!UP && conv_narrow_tiles() && wg128 < 512) return run_conv<64, 4, 1, CK, S, UP, EM>(p, st);
     return run_conv<128, 2, 2, CK, S, UP, EM>(p, st);
   }
 }

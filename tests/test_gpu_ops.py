@@ -273,6 +273,32 @@ def test_conv3x3(gpu, B, h, w, cin, cout, stride, relu_in, act, nres):
     close(nchw(out), ref, 1e-2, 1e-2, f"conv3x3 {h}x{w} {cin}->{cout} s{stride}")
 
 
+@pytest.mark.parametrize("h,cin,cout", [(148, 64, 64), (148, 256, 256), (75, 128, 128)])
+def test_conv_narrow_tiles_bit_exact(gpu, h, cin, cout):
+    """Batch-1 grids take narrower channel tiles (conv.hip conv_tiles: 32 of 64
+    channels, 64 of > 64): against torch, and bit for bit against the wide
+    tiles (MDE_CONV_NARROW=0) -- an output channel's K order is the tile's,
+    whatever the tile width."""
+    import os
+    x = rn(1, cin, h, h)
+    wt, b = rn(cout, cin, 3, 3, scale=(9 * cin) ** -0.5), rn(cout, scale=0.02)
+    ref = F.relu(F.conv2d(F.relu(x.half().float()), wt.half().float(), b, padding=1))
+    wp = conv_w(wt).to(gpu)
+    xg, bg = nhwc(x).half().to(gpu), b.to(gpu)
+    got = []
+    for flag in ("1", "0"):
+        os.environ["MDE_CONV_NARROW"] = flag
+        try:
+            out = torch.empty(1, h, h, cout, dtype=torch.float16, device=gpu)
+            op("mde_op_conv3x3", ptr(xg), 1, h, h, cin, ptr(wp), wp.shape[1], cout, 1, 1, ptr(bg), 1, None, None,
+               ptr(out), stream())
+        finally:
+            os.environ.pop("MDE_CONV_NARROW", None)
+        got.append(out)
+    close(nchw(got[0]), ref, 1e-2, 1e-2, f"conv narrow tiles {h}^2 {cin}->{cout}")
+    assert torch.equal(got[0], got[1]), "narrow conv tiles must equal the wide ones bit for bit"
+
+
 # E_STORE split-K (launch_gemm's small-grid policy): the batch-1 ViT-L DPT
 # shapes -- layer4_rn (19^2, 1024 -> 256, im2col), layer3_rn (37^2, direct conv
 # grid), conv_s2 (37^2 -> 19^2, stride 2), an RCU conv with pre-ReLU, bias,
