@@ -180,6 +180,32 @@ def test_attention_key_groups(gpu, cfg, B, H, T, spiky):
     close(o, ref, 2e-2, 5e-3, f"attention {cfg} B{B} H{H} T{T}")
 
 
+@pytest.mark.parametrize("cfg", ["8", "4", "8q2", "4q2", "8r3", "4r4", "4s2", "4s3"])
+@pytest.mark.parametrize("B,H,T", [(2, 3, 300), (1, 6, 1370)])
+def test_attention_tuning_configs(gpu, cfg, B, H, T):
+    """Every launch shape MDE_ATTN_CFG can force (mde_op_attention_cfg): 8 / 4
+    waves, two query sub-tiles per wave (q2), 3- and 4-deep K/V rings, split-KV
+    over workgroups with the combine kernel -- the same numbers as the policy's
+    shapes, against torch."""
+    Tp = -(-T // 64) * 64
+    q = rn(B * H, T, 64) * 0.125 * 2.0 * LOG2E
+    k = rn(B * H, T, 64) * 2.0
+    v = rn(B * H, T, 64)
+    ref = attn_ref(q, k, v).reshape(B, H, T, 64).permute(0, 2, 1, 3).reshape(B * T, H * 64)
+    qg = torch.zeros(B * H, Tp, 64, dtype=torch.float16, device=gpu)
+    kg = torch.zeros_like(qg)
+    vtg = torch.zeros(B * H, 64, Tp, dtype=torch.float16, device=gpu)
+    qg[:, :T], kg[:, :T] = q.half().to(gpu), k.half().to(gpu)
+    vtg[:, :, vt_perm(T).to(gpu)] = v.transpose(1, 2).half().to(gpu)
+    from monocular_depth_estimation_trt_amd import _lib
+    nbytes = _lib.lib().mde_op_attention_ws_bytes(B, H, T)
+    ws = torch.empty(max(nbytes, 4) // 4, dtype=torch.float32, device=gpu)
+    o = torch.empty(B * T, H * 64, dtype=torch.float16, device=gpu)
+    op("mde_op_attention_cfg", ptr(qg), ptr(kg), ptr(vtg), ptr(o), B, H, T, Tp, H * 64, cfg.encode(), ptr(ws),
+       nbytes, stream())
+    close(o, ref, 2e-2, 5e-3, f"attention cfg {cfg} B{B} H{H} T{T}")
+
+
 def test_attention_spiky_rows(gpu):
     """Force the online-softmax rescale: one key dominates late in the row."""
     B, H, T = 1, 2, 300
