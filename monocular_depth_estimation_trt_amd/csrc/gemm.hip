@@ -513,7 +513,6 @@ int tile_override() {
     if (!strcmp(e, "256x128w8")) return 4;  // 8 waves, BK 32 x 3 stages, two workgroups per CU
     if (!strcmp(e, "128x128w8")) return 5;  // 8 waves (2 x 4 of 64 x 32) on the 128^2 tile, any grid
     if (!strcmp(e, "big1")) return 6;       // small grids: tall tiles, 3-deep ring, one workgroup per CU
-    if (!strcmp(e, "w8b32")) return 7;      // the short-K dense stores' BK 32 128^2 tiles on 8 waves
     return 0;
   }
 }
@@ -623,7 +622,6 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
       // staging passes, proj 0.43 -> 0.45 even with f16 staging of the
       // update; ViT-L B=8 qkv 2.56 -> 2.67)
       if constexpr (AM == A_DENSE && (EM == E_STORE || EM == E_QKV)) {
-        if (p.K <= bk32_kmax() && bk32_tiles() && tile_override() == 7) return run<128, 128, 2, 4, AM, EM, 32>(p, st);
         if (p.K <= bk32_kmax() && bk32_tiles()) return run<128, 128, 2, 2, AM, EM, 32>(p, st);
         if (w8small(big)) return run<128, 128, 2, 4, AM, EM>(p, st);
       }
