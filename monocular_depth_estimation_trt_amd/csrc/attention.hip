@@ -147,8 +147,9 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
   constexpr int BQ = QW * NWQ * QS;  // queries per workgroup
   constexpr int INS = 8 / NWQ;       // glds instructions per wave per image (8 per 64-row image)
   constexpr int PER_TILE = 2 * INS;  // vmcnt entries one tile adds per wave (K + V^T)
-  static_assert(NWQ * NS == NW && (NWQ == 1 || NWQ == 2 || NWQ == 4 || NWQ == 8), "waves per key group");
-  static_assert(NW == 4 || NW == 8 || (NS > 1 && (NW == 12 || NW == 16)), "waves per workgroup");
+  static_assert(NWQ * NS == NW && (NWQ == 1 || NWQ == 2 || NWQ == 4 || NWQ == 8 || (NWQ == 3 && R == 2)),
+                "waves per key group");
+  static_assert(NW == 4 || NW == 8 || (NS > 1 && (NW == 6 || NW == 12 || NW == 16)), "waves per workgroup");
   static_assert(R >= 2 && R <= 4, "ring depth");
   constexpr int DIST = R - 1;  // tiles in flight ahead of the one computed
   constexpr int RING_B = R * NS * SLOT, MERGE_B = (NS - 1) * NWQ * MERGE_WAVE_B;
@@ -201,8 +202,11 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
     char* sK = gsm + slot * NS * SLOT;
     char* sV = sK + TILE_B;
 #pragma unroll
-    for (int i = 0; i < INS; ++i) {
-      const int g = wave * INS + i;  // 8-row group 0..7
+    for (int i = 0; i < (8 + NWQ - 1) / NWQ; ++i) {
+      // 8-row group 0..7: wave w takes w, w + NWQ, ... (3 query waves: 3 / 3 / 2;
+      // an uneven count is fine here -- the rings that allow NWQ = 3 wait vmcnt(0))
+      const int g = wave + i * NWQ;
+      if (8 % NWQ && g >= 8) break;
       const int row = g * 8 + lrow;
       const int lc = pc ^ ((row >> 1) & 7);
       __builtin_amdgcn_global_load_lds(kb + (size_t)(kt * KT + row) * 64 + lc * 8, sK + g * 8 * 128, 16, 0, 0);
@@ -578,7 +582,7 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
     const char* gp = strchr(forced, 'g');  // "<waves>g<groups>": in-workgroup key groups
     if (gp) groups = atoi(gp + 1);
   }
-  if (nw != 4 && nw != 8 && !(groups > 1 && (nw == 12 || nw == 16))) {
+  if (nw != 4 && nw != 8 && !(groups > 1 && (nw == 6 || nw == 12 || nw == 16))) {
     // 256-query workgroups share each K/V^T tile over 8 waves once the grid
     // fills the chip (2 per CU); smaller grids take 128-query groups and,
     // below one group per CU, split the keys -- at least 7 key tiles per
@@ -613,6 +617,7 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
     if (nw == 8 && groups == 2) return run_attn_grp<8, 2>(q, k, vt, o, B, H, T, Tpad, ldo, st);
     if (nw == 8 && groups == 4) return run_attn_grp<8, 4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
     if (nw == 12 && groups == 3) return run_attn_grp<12, 3>(q, k, vt, o, B, H, T, Tpad, ldo, st);
+    if (nw == 6 && groups == 2) return run_attn_grp<6, 2>(q, k, vt, o, B, H, T, Tpad, ldo, st);
     if (nw == 16 && groups == 4) return run_attn_grp<16, 4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
   }
   if (nw == 8 && qs2 && split <= 1) return run_attn<8, 2, 2>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, 1, st);

@@ -233,6 +233,9 @@ size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
   t.aws = t.aws_bytes ? a.f(t.aws_bytes / sizeof(float)) : nullptr;
   t.sws = a.f(kSplitWsFloats);
   t.sws2 = a.f(kSplitWsFloats);
+  // stream-K (batch-1 encoder linears whose 128^2 grid overhangs the CUs)
+  t.skws = bb * e.T <= 4096 ? a.f(kSkWsFloats) : nullptr;
+  t.skcnt = t.skws ? (int*)a.take(kSkMaxTiles * sizeof(int)) : nullptr;
   if (b) *b = t;
   return a.off;
 }
@@ -282,6 +285,8 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
 
   const bool fold = b.st != nullptr;
   split_ws = b.sws;
+  sk_ws = b.skws;
+  sk_cnt = b.skcnt;
   const float* cls_st = fold ? w32("pos.cls.st") : nullptr;
   step("patch_prep", [&] {
     if (cf.input_u8)
@@ -390,11 +395,14 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
     if ((err = hipStreamWaitEvent(c.side_stream, c.fork_ev[i], 0)) != hipSuccess) return;
     const hipStream_t main_st = st;
     float* const main_ws = split_ws;
+    float* const main_sk = sk_ws;
     st = c.side_stream;
     split_ws = b.sws2;
+    sk_ws = nullptr;  // the stream-K workspace stays with the main stream
     reassemble(i);
     st = main_st;
     split_ws = main_ws;
+    sk_ws = main_sk;
   };
 
   int tap = 0;

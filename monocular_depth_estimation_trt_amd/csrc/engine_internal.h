@@ -40,6 +40,8 @@ struct DAV2Buf {
   float* st;        // folded-LN partials [B*T][D/32][2] (f16 residual + folded pack, else null)
   float* sws;       // E_STORE split-K partials (GemmParams::partial_cap = kSplitWsFloats)
   float* sws2;      // the same for the reassemble branch forked onto the side stream
+  float* skws;      // stream-K partial tiles (GemmParams::sk_ws; small-batch contexts only, else null)
+  int* skcnt;       // stream-K tile arrival counters (zeroed with the arena)
 };
 
 // fp32 elements of a context's E_STORE split-K workspace (launch_gemm bounds
@@ -276,16 +278,21 @@ struct Runner {
 
   // E_STORE split-K workspace for launch_gemm's small-grid policy (null: never split)
   float* split_ws = nullptr;
+  // stream-K workspace of the main stream (null: never stream-K)
+  float* sk_ws = nullptr;
+  int* sk_cnt = nullptr;
 
   void gemm(const char* name, const GemmParams& g) {
+    GemmParams q = g;
     if (split_ws && g.emode == E_STORE && !g.partial) {
-      GemmParams q = g;
       q.partial = split_ws;
       q.partial_cap = kSplitWsFloats;
-      step(name, [&] { return launch_gemm(q, st); });
-      return;
     }
-    step(name, [&] { return launch_gemm(g, st); });
+    if (!q.sk_ws) {
+      q.sk_ws = sk_ws;
+      q.sk_cnt = sk_cnt;
+    }
+    step(name, [&] { return launch_gemm(q, st); });
   }
 
   // pre-activation residual conv unit:

@@ -88,7 +88,15 @@ struct GemmParams {
   // partial row) (m / (a_tok - 1)) * a_tok + 1 + m % (a_tok - 1), i.e. every
   // sequence's first (cls) row is skipped
   int a_tok = 0;
+  // stream-K workspace (batch-1 grids, gemm.hip gemm_sk_kernel): sk_ws =
+  // fp32 [2 * 2 * kSkMaxWG][128 * 128] partial tiles, sk_cnt = kSkMaxTiles int
+  // arrival counters, zero-initialised and left zero by every launch; null:
+  // never stream-K.  The workspace belongs to one stream at a time.
+  float* sk_ws = nullptr; int* sk_cnt = nullptr;
 };
+constexpr int kSkMaxWG = 256;
+constexpr int kSkMaxTiles = 4096;
+constexpr size_t kSkWsFloats = size_t(2) * 2 * kSkMaxWG * 128 * 128;  // two slots per workgroup, two workgroups per CU
 
 // x32[m*ldo+n] += ls[n] * (sum_{s<S} P[s][m][n] + bias[n]), slices summed in
 // order (elementwise.hip): the second half of the E_RESID split-K path

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--dim", type=int, default=384, help="ViT width D (ViT-L: 1024)")
     ap.add_argument("--heads", type=int, default=6, help="attention heads (ViT-L: 16)")
+    ap.add_argument("--tokens", type=int, default=1370, help="tokens per image (GEMM rows = batch x tokens)")
     ap.add_argument("--cold", action="store_true",
                     help="also time each launch alone after a 512 MB write (caches cold, as in the graph)")
     a = ap.parse_args()
@@ -32,7 +33,7 @@ def main():
     from gpu_util import conv_w, pad_w, ptr, stream
     from monocular_depth_estimation_trt_amd import _lib
     dev = torch.device("cuda:0")
-    B, T, D, H = a.batch, 1370, a.dim, a.heads
+    B, T, D, H = a.batch, a.tokens, a.dim, a.heads
     M = B * T
     g = torch.Generator(device=dev).manual_seed(0)
 
@@ -83,7 +84,7 @@ def main():
         w = pad_w(rnd(n, k, scale=k ** -0.5))
         timeit(name, lambda: L.mde_op_linear_residual(ptr(x16), k, ptr(w), w.shape[1], M, n, k, ptr(bias), ptr(ls),
                                                       ptr(x32), D, st), 2.0 * M * n * k)
-    Tp = 1408
+    Tp = (T + 63) // 64 * 64
     w = pad_w(rnd(3 * D, D, scale=D ** -0.5))
     q = torch.zeros(B * H, Tp, 64, dtype=torch.float16, device=dev)
     k_ = torch.zeros_like(q)
@@ -97,7 +98,7 @@ def main():
     k_.normal_()
     vt.normal_()
     o = torch.empty(M, D, dtype=torch.float16, device=dev)
-    timeit(f"attention T1370 H{H}", lambda: L.mde_op_attention(ptr(q), ptr(k_), ptr(vt), ptr(o), B, H, T, Tp, D, st),
+    timeit(f"attention T{T} H{H}", lambda: L.mde_op_attention(ptr(q), ptr(k_), ptr(vt), ptr(o), B, H, T, Tp, D, st),
            4.0 * B * H * T * T * 64)
     F = 64
     for hw in (148, 74):
