@@ -389,7 +389,9 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
           }
           m2 += __shfl_xor(m2, 16);
           m2 += __shfl_xor(m2, 32);
-          if ((lane >> 4) == 0) *reinterpret_cast<float2*>(smem + SG * STAGE + r * 8) = make_float2(mean, m2 * invd);
+          // (RPW 8, 16-wave tiles: lanes 8..15 repeat the next wave's rows)
+          if ((lane >> 4) == 0 && (RPW >= 16 || (lane & 15) < RPW))
+            *reinterpret_cast<float2*>(smem + SG * STAGE + r * 8) = make_float2(mean, m2 * invd);
         }
       }
     }
@@ -798,6 +800,13 @@ bool w8small(long long wgs) {
   return wgs < 512;
 }
 
+// MDE_GEMM_W16=1: 16 waves (4 x 4 of 32 x 32) on those small-grid 128^2
+// tiles instead of 8 (tuning; read per launch)
+bool w16small() {
+  const char* e = getenv("MDE_GEMM_W16");
+  return e && e[0] == '1';
+}
+
 // 128^2 tiles once the grid holds at least this many of them (MDE_GEMM_BIG_MIN: tuning)
 long long big_tile_min() {
   static const long long v = [] {
@@ -883,6 +892,7 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
       // update; ViT-L B=8 qkv 2.56 -> 2.67)
       if constexpr (AM == A_DENSE && (EM == E_STORE || EM == E_QKV)) {
         if (p.K <= bk32_kmax() && bk32_tiles()) return run<128, 128, 2, 2, AM, EM, 32>(p, st);
+        if (w16small() && w8small(big)) return run<128, 128, 4, 4, AM, EM>(p, st);
         if (w8small(big)) return run<128, 128, 2, 4, AM, EM>(p, st);
       }
       return run<128, 128, 2, 2, AM, EM>(p, st);

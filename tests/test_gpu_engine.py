@@ -218,11 +218,13 @@ def test_dpt_fork_bit_exact(gpu, encoder, size, B):
     assert np.array_equal(y_fork_eager, y_one), "forked DPT branch (eager) must equal the one-stream forward"
 
 
-@pytest.mark.parametrize("tile", ["big1", "128x128w8"])
-def test_gemm_tile_variants_bit_exact(gpu, tile):
+@pytest.mark.parametrize("var,tile", [("MDE_GEMM_TILE", "big1"), ("MDE_GEMM_TILE", "128x128w8"),
+                                      ("MDE_GEMM_W16", "1")])
+def test_gemm_tile_variants_bit_exact(gpu, var, tile):
     """ViT-L 518^2 B=1 (config 3's unit) with the small-grid GEMM tilings
     (MDE_GEMM_TILE: tall 160/192-row tiles on a 3-deep ring, or 8 waves on
-    the 128^2 tile).  A tile's K loop runs in the same order whatever its
+    the 128^2 tile; MDE_GEMM_W16: 16 waves of 32 x 32 on the small-grid
+    128^2 tiles).  A tile's K loop runs in the same order whatever its
     shape and the split-K slicing is unchanged, so the depth map must equal
     the default tiling's bit for bit."""
     cfg = weights.model_config("vitl", "metric")
@@ -230,13 +232,13 @@ def test_gemm_tile_variants_bit_exact(gpu, tile):
     blob = pack.pack_bytes(sd, cfg, 518, 518)
     x = weights.synthetic_images(1, 518, 518, first_seed=51)
     y_def = run_engine(blob, x)
-    os.environ["MDE_GEMM_TILE"] = tile
+    os.environ[var] = tile
     try:
         y_var = run_engine(blob, x)
     finally:
-        os.environ.pop("MDE_GEMM_TILE", None)
+        os.environ.pop(var, None)
     assert np.isfinite(y_def).all()
-    assert np.array_equal(y_var, y_def), f"MDE_GEMM_TILE={tile} changed the result"
+    assert np.array_equal(y_var, y_def), f"{var}={tile} changed the result"
 
 
 @pytest.mark.parametrize("encoder,head", [("vitl", "metric"), ("vitl", "relative")])
