@@ -775,6 +775,7 @@ int tile_override() {
     if (!strcmp(e, "256x128w8")) return 4;  // 8 waves, BK 32 x 3 stages, two workgroups per CU
     if (!strcmp(e, "128x128w8")) return 5;  // 8 waves (2 x 4 of 64 x 32) on the 128^2 tile, any grid
     if (!strcmp(e, "big1")) return 6;       // small grids: tall tiles, 3-deep ring, one workgroup per CU
+    if (!strcmp(e, "64x128w8")) return 7;   // small grids: 64 x 128 tiles, 8 waves, three workgroups per CU
     return 0;
   }
 }
@@ -892,6 +893,7 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
       // update; ViT-L B=8 qkv 2.56 -> 2.67)
       if constexpr (AM == A_DENSE && (EM == E_STORE || EM == E_QKV)) {
         if (p.K <= bk32_kmax() && bk32_tiles()) return run<128, 128, 2, 2, AM, EM, 32>(p, st);
+        if (tile_override() == 7 && w8small(big)) return run<64, 128, 2, 4, AM, EM>(p, st);
         if (w16small() && w8small(big)) return run<128, 128, 4, 4, AM, EM>(p, st);
         if (w8small(big)) return run<128, 128, 2, 4, AM, EM>(p, st);
       }

@@ -223,8 +223,8 @@ def test_dpt_fork_bit_exact(gpu, encoder, size, B):
 def test_gemm_tile_variants_bit_exact(gpu, var, tile):
     """ViT-L 518^2 B=1 (config 3's unit) with the small-grid GEMM tilings
     (MDE_GEMM_TILE: tall 160/192-row tiles on a 3-deep ring, or 8 waves on
-    the 128^2 tile; MDE_GEMM_W16: 16 waves of 32 x 32 on the small-grid
-    128^2 tiles).  A tile's K loop runs in the same order whatever its
+    the 128^2 tile, or 64 x 128 small-grid tiles; MDE_GEMM_W16: 16 waves of
+    32 x 32 on the small-grid 128^2 tiles).  A tile's K loop runs in the same order whatever its
     shape and the split-K slicing is unchanged, so the depth map must equal
     the default tiling's bit for bit."""
     cfg = weights.model_config("vitl", "metric")
