@@ -45,6 +45,7 @@ Also measured (rank 0):
 from __future__ import annotations
 
 import argparse
+import gc
 import json
 import os
 import statistics
@@ -204,13 +205,28 @@ def b1_reference_method(blob, dev, images, warmup, iters, ref_fps, prefix="b1_")
     fn = lambda: cr.do_inference(ctx, eng, bindings, inputs, outputs, stream, timer=timer)  # noqa: E731
     for _ in range(warmup):
         fn()
+    # host-side pauses inside the timed loop: Python's cyclic GC (a gen-2 pass
+    # walks every object torch created, milliseconds) -- recorded per sample
+    gc_log = []
+    t_gc = [0.0]
+
+    def _gc_cb(phase, info):
+        if phase == "start":
+            t_gc[0] = time.perf_counter()
+        else:
+            gc_log.append((len(samples), info.get("generation"), (time.perf_counter() - t_gc[0]) * 1e3))
+
     samples, stages = [], {k: [] for k in cr.StageTimer.STAGES}
-    for _ in range(iters):
-        t0 = time.perf_counter()
-        fn()
-        samples.append((time.perf_counter() - t0) * 1e3)
-        for k, v in timer.last.items():
-            stages[k].append(v)
+    gc.callbacks.append(_gc_cb)
+    try:
+        for _ in range(iters):
+            t0 = time.perf_counter()
+            fn()
+            samples.append((time.perf_counter() - t0) * 1e3)
+            for k, v in timer.last.items():
+                stages[k].append(v)
+    finally:
+        gc.callbacks.remove(_gc_cb)
     out = outputs[0].host.copy()
     timer.free()
     cr.free_buffers(inputs, outputs, stream)
@@ -219,8 +235,12 @@ def b1_reference_method(blob, dev, images, warmup, iters, ref_fps, prefix="b1_")
     mean = statistics.fmean(samples)
     s = sorted(samples)
     pct = lambda q: s[min(len(s) - 1, max(0, int(np.ceil(q / 100 * len(s))) - 1))]  # noqa: E731
+    imax = int(np.argmax(samples))
     res = {"mean_ms": round(mean, 4), "p50_ms": round(pct(50), 4), "p99_ms": round(pct(99), 4),
-           "fps": round(1000.0 / mean, 2), "vs_ref_fps": round(1000.0 / mean / ref_fps, 3)}
+           "max_ms": round(samples[imax], 4), "max_iter": imax,
+           "fps": round(1000.0 / mean, 2), "vs_ref_fps": round(1000.0 / mean / ref_fps, 3),
+           "max_iter_stages": {k: round(v[imax], 4) for k, v in stages.items() if len(v) > imax},
+           "gc_in_loop": [[i, g, round(ms, 3)] for i, g, ms in gc_log]}
     for k, v in stages.items():
         res[k] = round(statistics.fmean(v), 4)
     res["out_mean"] = float(out.mean())

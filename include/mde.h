@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MDE_ABI_VERSION 5
+#define MDE_ABI_VERSION 6
 
 typedef enum {
   MDE_OK = 0,
@@ -91,6 +91,21 @@ typedef void (*mde_layer_cb)(const char* layer_name, float ms, void* user);
 /* ---- library ---------------------------------------------------------- */
 int mde_version(void);
 const char* mde_last_error(void);
+/* Dispatch switches (no reference counterpart: TensorRT picks tactics at build
+ * time).  Each starts at its default, is overridden once per process from the
+ * environment variable MDE_<NAME>, and can be changed here afterwards; a
+ * captured hipGraph keeps the choice it was captured with.  Names (range,
+ * default): "splitk" (0-1, 1) split-K of small-grid GEMMs / DPT convs;
+ * "lnfold" (0-1, 1) LayerNorm folded into the consumer GEMMs, read at context
+ * creation; "conv_narrow" (0-1, 1) narrow conv channel tiles on small grids;
+ * "upconv" (0-1, 1) separable upsampling head conv; "gemm256" (0-2, 1) 256^2
+ * GEMM tiles (0 never, 1 auto, 2 always); "deep64" (0-1, 1) 4-deep ring for
+ * small-grid 64^2 tiles; "w8small" (0-1, 1) 8-wave small-grid 128^2 tiles.
+ * Every setting computes the same depth map within the stated tolerance; the
+ * tile switches are bit-identical.  MDE_ERR_NAME: unknown name; MDE_ERR_ARG:
+ * value out of range. */
+int mde_tuning_set(const char* name, int value);
+int mde_tuning_get(const char* name, int* value);
 
 /* ---- engine (replaces get_engine / ICudaEngine) ----------------------- */
 int mde_engine_load(const char* packed_path, int device, mde_engine** out);
@@ -181,9 +196,10 @@ int mde_op_attention_ws(const void* q_f16, const void* k_f16, const void* vt_f16
                         int tokens, int tokens_pad, int ldo, void* ws, size_t ws_bytes, void* stream);
 size_t mde_op_attention_ws_bytes(int batch, int heads, int tokens);
 /* mde_op_attention_ws with an explicit launch configuration (tests / tuning; no reference
- * counterpart): cfg = "<waves>[s<split>][g<groups>]", e.g. "8" (256-query workgroups), "4s2"
- * (split-KV over two workgroups + merge kernel, needs ws), "4g2" (two key groups of 64 queries
- * inside one workgroup, merged through LDS); NULL or "" = the launcher's policy. */
+ * counterpart): cfg = "<waves>[s<split>][g<groups>][r<ring>][q2]", e.g. "8" (256-query
+ * workgroups), "4s2" (split-KV over two workgroups + merge kernel, needs ws), "4g2" (two key
+ * groups of 64 queries inside one workgroup, merged through LDS); NULL or "" = the launcher's
+ * policy. */
 int mde_op_attention_cfg(const void* q_f16, const void* k_f16, const void* vt_f16, void* o_f16, int batch, int heads,
                          int tokens, int tokens_pad, int ldo, const char* cfg, void* ws, size_t ws_bytes,
                          void* stream);

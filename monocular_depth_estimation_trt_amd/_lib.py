@@ -8,6 +8,7 @@ parity claim.
 
 from __future__ import annotations
 
+import contextlib
 import ctypes as C
 import os
 import threading
@@ -47,6 +48,8 @@ LAYER_CB = C.CFUNCTYPE(None, c_char_p, c_float, c_void_p)
 PROTOTYPES = {
     "mde_version": [],
     "mde_last_error": [],
+    "mde_tuning_set": [c_char_p, c_int],
+    "mde_tuning_get": [c_char_p, P(c_int)],
     "mde_engine_load": [c_char_p, c_int, P(c_void_p)],
     "mde_engine_load_memory": [c_void_p, c_size_t, c_int, P(c_void_p)],
     "mde_engine_destroy": [c_void_p],
@@ -139,6 +142,43 @@ class MDEError(RuntimeError):
         super().__init__(f"{fn} failed ({STATUS.get(code, code)}): {msg}")
 
 
+def hip_runtimes() -> list:
+    """The distinct libamdhip64 images mapped into this process (from
+    /proc/self/maps; empty where that is not readable)."""
+    paths = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                parts = line.split(None, 5)
+                if len(parts) == 6 and "libamdhip64" in os.path.basename(parts[5].strip()):
+                    paths.add(os.path.realpath(parts[5].strip()))
+    except OSError:
+        return []
+    return sorted(paths)
+
+
+def check_single_runtime() -> None:
+    """Raise if two HIP runtimes are mapped into this process.
+
+    Root cause (established on this image): PyTorch-ROCm's bundled
+    torch/lib/libamdhip64.so and ROCm's /opt/rocm/lib/libamdhip64.so.7 both
+    carry the SONAME libamdhip64.so.7.  libmde_hip.so NEEDs that soname, so
+    when torch is loaded first the dynamic loader binds libmde_hip to torch's
+    runtime (one runtime: torch's streams and ours are the same objects).
+    When libmde_hip is loaded first it maps ROCm's copy, and a later torch
+    import NEEDs "libamdhip64.so" -- no soname match -- and maps a second
+    runtime: each initialises its own HSA runtime, ours then sees no device
+    (hipSetDevice: no ROCm-capable device), and a hipStream_t that torch hands
+    across the ABI would belong to the other runtime.  Nothing works reliably
+    in that state, so fail loudly instead."""
+    rts = hip_runtimes()
+    if len(rts) > 1:
+        raise ImportError(
+            "two HIP runtimes are loaded in this process (" + ", ".join(rts) + "): libmde_hip.so was loaded "
+            "before PyTorch's bundled HIP runtime.  Import torch (and call torch.cuda.is_available()) before "
+            "loading libmde_hip.so, or do not load torch in a process that uses libmde_hip.so directly.")
+
+
 def lib() -> C.CDLL:
     """Load libmde_hip.so once; raise loudly if it is not there."""
     global _lib
@@ -151,18 +191,17 @@ def lib() -> C.CDLL:
                     f"libmde_hip.so not found at {LIB_PATH}. Build it first: "
                     f"python -c 'import __graft_entry__ as g; g.build()' (or "
                     f"python -m monocular_depth_estimation_trt_amd._build). There is no CPU fallback.")
-            # PyTorch-ROCm wheels bundle their own libamdhip64: with two HIP
-            # runtimes in one process, ours finds no device when it is loaded
-            # before torch's runtime has come up and initialised after it
-            # (measured on the MI355X box: build() then smoke() in one process
-            # failed hipSetDevice; torch first, or ours loaded after torch's
-            # init, works).  Bring torch's runtime up first when torch is here.
+            # One HIP runtime per process (check_single_runtime): when torch
+            # is importable, bring its bundled runtime up first so that
+            # libmde_hip binds to it and the streams torch hands over are the
+            # runtime's own.
             try:
                 import torch
                 torch.cuda.is_available()
             except ImportError:
                 pass
             L = C.CDLL(LIB_PATH)
+            check_single_runtime()
             for name, args in PROTOTYPES.items():
                 f = getattr(L, name)
                 f.argtypes = args
@@ -181,6 +220,36 @@ def call(name: str, *args) -> None:
     rc = getattr(lib(), name)(*args)
     if rc != MDE_OK:
         raise MDEError(name, rc, last_error())
+
+
+TUNING = ("splitk", "lnfold", "conv_narrow", "upconv", "gemm256", "deep64", "w8small")
+
+
+def get_tuning(name: str) -> int:
+    v = c_int()
+    call("mde_tuning_get", name.encode(), C.byref(v))
+    return v.value
+
+
+def set_tuning(name: str, value: int) -> None:
+    """Set a dispatch switch of the library (include/mde.h mde_tuning_set)."""
+    rc = lib().mde_tuning_set(name.encode(), int(value))
+    if rc != MDE_OK:
+        raise ValueError(f"mde_tuning_set({name!r}, {value}) failed ({STATUS.get(rc, rc)}): "
+                         f"known switches {TUNING}")
+
+
+@contextlib.contextmanager
+def tuning(**switches):
+    """Temporarily set dispatch switches: `with tuning(splitk=0): ...`."""
+    old = {k: get_tuning(k) for k in switches}
+    try:
+        for k, v in switches.items():
+            set_tuning(k, v)
+        yield
+    finally:
+        for k, v in old.items():
+            set_tuning(k, v)
 
 
 def exported_symbols():

@@ -36,7 +36,7 @@
 // waves, each group streaming its own slice of the key tiles through its own
 // ring slots, the groups' (O, m, l) merged through LDS after the loop (ViT-L
 // B=1: 2 groups of 128 queries; ViT-S B=1: 4 groups of 64).  Fallback (grids
-// too large for that, MDE_ATTN_CFG "4s<n>"): over gridDim.z, each split
+// too large for that, cfg "4s<n>"): over gridDim.z, each split
 // writing its unnormalised fp32 O with its running max and sum for
 // attn_combine_kernel to merge.
 //
@@ -46,7 +46,7 @@
 // second half (waves 4-7 half a tile behind, carrying the scores across the
 // barrier: 155 vs 113 us at 226 VGPRs / one workgroup per CU, and 117-120 vs
 // 112-114 us with one loop per wave role at 128 VGPRs / two per CU) were all
-// slower than this form; 3- and 4-deep K/V rings (MDE_ATTN_CFG=8r3 / 8r4) measure
+// slower than this form; 3- and 4-deep K/V rings (cfg "8r3" / "8r4") measure
 // the same as 2 (SQ counters: the waits are issue/dependency stalls, not
 // load latency).
 #include <cstdlib>
@@ -568,9 +568,9 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
   // the 16-B output stores need ldo % 8 == 0 (and a 16-B aligned o)
   if (Tpad % KT || Tpad < ((T + KT - 1) / KT) * KT || (ldo & 7) || ((uintptr_t)o & 15)) return hipErrorInvalidValue;
   const int nkt = (T + KT - 1) / KT;
-  // MDE_ATTN_CFG = <waves>[s<split>][r<ring>] ("8", "4", "4s8", "8r3", ...): tuning override
-  static const char* env_cfg = getenv("MDE_ATTN_CFG");
-  const char* forced = cfg && cfg[0] ? cfg : env_cfg;
+  // cfg = <waves>[s<split>][g<groups>][r<ring>][q2] ("8", "4", "4s8", "8r3", ...):
+  // a forced launch shape (mde_op_attention_cfg: tests, tuning)
+  const char* forced = cfg && cfg[0] ? cfg : nullptr;
   int nw = 0, split = 1, ring = ATTN_RING, qs2 = 0, groups = 1;
   if (forced) {
     nw = atoi(forced);

@@ -19,6 +19,7 @@
 #include "mde_device.h"
 #include "mde_ops.h"
 #include "tile_epilogue.h"
+#include "tuning.h"
 
 #ifndef MDE_EPI_LDS
 #define MDE_EPI_LDS 1  // row-major epilogue staged through LDS (whole-line stores)
@@ -337,16 +338,13 @@ hipError_t run_conv(const GemmParams& p, hipStream_t st) {
   return hipGetLastError();
 }
 
-// Narrower channel tiles for small grids (MDE_CONV_NARROW=0 turns them off,
-// read per call): wide convs (N > 64) whose 128-channel grid leaves CUs with
+// Narrower channel tiles for small grids (switch "conv_narrow", tuning.h):
+// wide convs (N > 64) whose 128-channel grid leaves CUs with
 // one or two workgroups (under 512: batch 1, e.g. ViT-L's 148^2 256-channel
 // RCUs at 380) take 64-channel tiles -- twice the workgroups at 40 KB LDS
 // each, the busiest CU carrying ~3 half-width tiles instead of 2 full ones;
 // 64-channel convs under one workgroup per CU take 32-channel tiles.
-bool conv_narrow_tiles() {
-  const char* e = getenv("MDE_CONV_NARROW");
-  return !(e && e[0] == '0');
-}
+bool conv_narrow_tiles() { return knob(KNOB_CONV_NARROW) != 0; }
 
 template <int CK, int S, bool UP, int EM>
 hipError_t conv_tiles(const GemmParams& p, hipStream_t st) {
@@ -679,12 +677,8 @@ upconv_kernel(const GemmParams p) {
   }
 }
 
-// MDE_UPCONV=0: the upsampling convs stay on conv3_kernel (A/B; read per
-// call so a test can compare both kernels -- captured graphs keep their choice)
-bool upconv_enabled() {
-  const char* e = getenv("MDE_UPCONV");
-  return !(e && e[0] == '0');
-}
+// switch "upconv" = 0: the upsampling convs stay on conv3_kernel (A/B, tests)
+bool upconv_enabled() { return knob(KNOB_UPCONV) != 0; }
 
 // a 16-row tile's 18 virtual rows must come from at most USR source rows:
 // (UPH - 1) * scale + 2 rows, with a one-row margin for the float index
@@ -697,22 +691,18 @@ bool upconv_eligible(const GemmParams& p) {
   return sy * (UPH - 1) + 3.0 <= (double)USR && upconv_enabled();
 }
 
-// persistent grid: workgroups per CU the LDS allows x 256 CUs (MDE_UPCONV_PERSIST=0: one tile per workgroup)
+// persistent grid: workgroups per CU the LDS allows x 256 CUs (grids up to
+// that size run one tile per workgroup)
 template <int NCH>
 int upconv_grid() {
   constexpr int lds = UPATCH + UHBUF + 9 * NCH * 32 * 64;
   const int per_cu = 163840 / lds < 4 ? 163840 / lds : 4;
   return 256 * (per_cu > 0 ? per_cu : 1);
 }
-bool upconv_persist() {
-  const char* e = getenv("MDE_UPCONV_PERSIST");
-  return !(e && e[0] == '0');
-}
-
 template <int NCH, int EM>
 void launch_upconv_n(const GemmParams& p, long long tiles, hipStream_t st) {
   const int grid = upconv_grid<NCH>();
-  if (upconv_persist() && tiles > grid)
+  if (tiles > grid)
     hipLaunchKernelGGL((upconv_kernel<NCH, EM, true>), dim3((unsigned)grid), dim3(512), 0, st, p);
   else
     hipLaunchKernelGGL((upconv_kernel<NCH, EM, false>), dim3((unsigned)tiles), dim3(512), 0, st, p);

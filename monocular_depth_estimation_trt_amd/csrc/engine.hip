@@ -156,28 +156,9 @@ int load_pack(const uint8_t* data, size_t n, int device, mde_engine** out) {
 namespace mde {
 
 // ---- DA-V2 activation arena ---------------------------------------------------
-// MDE_LNFOLD=0: norm1 / norm2 as LayerNorm launches + the unfolded linears (A/B, tests)
-bool lnfold_off() {
-  static const bool off = [] {
-    const char* e = getenv("MDE_LNFOLD");
-    return e && e[0] == '0';
-  }();
-  return off;
-}
-
-// Fork the DPT reassemble + layerN_rn work of taps 0..2 onto a side stream
-// while the encoder's remaining blocks run (small grids only: at most ~2
-// workgroups per CU in the encoder's widest GEMM).  Off unless MDE_DPT_FORK=1
-// (read per forward; a captured graph keeps its choice): measured slower on
-// MI355X -- ViT-L 518^2 B=1 3.66 -> 3.91 ms per forward, ViT-S B=1 0.90 ->
-// 1.11 ms (profiles/r03_v4_*): the branch's split-K convs fill the chip and
-// stretch the latency-bound encoder launches by more than they hide.
-bool dpt_fork(const mde_engine& e, int B) {
-  const char* s = getenv("MDE_DPT_FORK");
-  if (!(s && s[0] == '1')) return false;
-  const long long tiles = (long long)((B * e.T + 127) / 128) * ((e.cfg.mlp_hidden + 127) / 128);
-  return tiles <= 512;
-}
+// switch "lnfold" = 0 (tuning.h): norm1 / norm2 as LayerNorm launches + the
+// unfolded linears (A/B, tests); read when a context is created
+bool lnfold_off() { return knob(KNOB_LNFOLD) == 0; }
 
 size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
   ArenaPlan a(base);
@@ -202,15 +183,17 @@ size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
   t.Hn = a.h(bb * e.T * D);
   // LayerNorm folded into qkv / fc1 (packs with the folded weights): the
   // residual writers leave per-32-column (sum, sum of squares) partials here
-  t.st = (e.cfg.resid_f16 && D % 128 == 0 && D <= 1024 && e.get("pos.cls.st") && !lnfold_off())
-             ? a.f(bb * e.T * (D / 16))
-             : nullptr;
+  const bool fold = e.cfg.resid_f16 && D % 128 == 0 && D <= 1024 && e.get("pos.cls.st") && !lnfold_off();
+  t.st = fold ? a.f(bb * e.T * (D / 16)) : nullptr;
   t.Q = a.h(bb * e.H * e.Tpad * 64);
   t.K = a.h(bb * e.H * e.Tpad * 64);
   t.Vt = a.h(bb * e.H * e.Tpad * 64);
   t.O = a.h(bb * e.T * D);
   t.Mh = a.h(bb * e.T * e.cfg.mlp_hidden);
-  for (int i = 0; i < 4; ++i) t.tap[i] = a.h(bb * np * D);
+  // tap token maps: only without the tap-LayerNorm fold (the projects read
+  // the residual stream directly when proj*.wf is packed)
+  const bool fold_taps = fold && e.get("proj0.wf");
+  for (int i = 0; i < 4; ++i) t.tap[i] = fold_taps ? nullptr : a.h(bb * np * D);
   for (int i = 0; i < 4; ++i) t.pj[i] = a.h(bb * np * oc[i]);
   t.l1 = a.h(bb * s1 * e.c1p);  // channels padded to a multiple of 32 (pad stays 0)
   t.l2 = a.h(bb * s2 * oc[1]);
@@ -232,10 +215,6 @@ size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
   t.aws_bytes = bsplit >= 1 ? attention_split_ws_bytes(bsplit, e.H, e.T) : 0;
   t.aws = t.aws_bytes ? a.f(t.aws_bytes / sizeof(float)) : nullptr;
   t.sws = a.f(kSplitWsFloats);
-  t.sws2 = a.f(kSplitWsFloats);
-  // stream-K (batch-1 encoder linears whose 128^2 grid overhangs the CUs)
-  t.skws = bb * e.T <= 4096 ? a.f(kSkWsFloats) : nullptr;
-  t.skcnt = t.skws ? (int*)a.take(kSkMaxTiles * sizeof(int)) : nullptr;
   if (b) *b = t;
   return a.off;
 }
@@ -285,8 +264,6 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
 
   const bool fold = b.st != nullptr;
   split_ws = b.sws;
-  sk_ws = b.skws;
-  sk_cnt = b.skcnt;
   const float* cls_st = fold ? w32("pos.cls.st") : nullptr;
   step("patch_prep", [&] {
     if (cf.input_u8)
@@ -383,28 +360,6 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
     snprintf(nm, sizeof nm, "layer%d_rn", i + 1);
     gemm(nm, g);
   };
-  // Small grids: taps 0..2's reassemble branch runs on the side stream
-  // beside the encoder's later blocks (it reads only its tap map and writes
-  // only its own buffers; its split-K partials go to sws2), joined before
-  // the tap-3 branch and the fusion blocks.  Not under the per-layer
-  // profiler (one stream, so layer times stay attributable).
-  const bool fork = !prof && c.side_stream && b.sws2 && dpt_fork(e, B);
-  auto fork_reassemble = [&](int i) {
-    if (err != hipSuccess) return;
-    if ((err = hipEventRecord(c.fork_ev[i], st)) != hipSuccess) return;
-    if ((err = hipStreamWaitEvent(c.side_stream, c.fork_ev[i], 0)) != hipSuccess) return;
-    const hipStream_t main_st = st;
-    float* const main_ws = split_ws;
-    float* const main_sk = sk_ws;
-    st = c.side_stream;
-    split_ws = b.sws2;
-    sk_ws = nullptr;  // the stream-K workspace stays with the main stream
-    reassemble(i);
-    st = main_st;
-    split_ws = main_ws;
-    sk_ws = main_sk;
-  };
-
   int tap = 0;
   for (int i = 0; i < cf.depth; ++i) {
     const std::string p = "b" + std::to_string(i) + ".";
@@ -412,11 +367,10 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
     // small batch: fc2's 64^2 tiles do not fill the chip and each walks a
     // K = 4D loop -- split K (B = 1: ViT-S 132 tiles x 4, ViT-L 352 x 2;
     // ViT-L fc2 1.23 -> 0.88 ms per forward; proj at K = 1024 gained
-    // nothing); MDE_SPLITK=0 turns it off (A/B, tests)
+    // nothing); switch "splitk" = 0 turns it off (A/B, tests)
     auto split_k = [&](GemmParams& g, int K) {
       const long long t64 = (long long)((B * T + 63) / 64) * ((D + 63) / 64);
-      const char* sk = getenv("MDE_SPLITK");
-      if (b.ws && t64 < 512 && K >= 1024 && !(sk && sk[0] == '0')) {
+      if (b.ws && t64 < 512 && K >= 1024 && knob(KNOB_SPLITK)) {
         g.partial = b.ws;
         g.splitk = t64 < 256 ? 4 : 2;
       }
@@ -519,18 +473,11 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
           return launch_layernorm(b.X, dst, w32("norm.g"), w32("norm.b"), B * T, D, cf.ln_eps, T, 1, st, b.Xh);
         });
       }
-      if (fork && tap < 3) fork_reassemble(tap);
       ++tap;
     }
   }
   if (tap != 4) return hipErrorInvalidValue;
-  if (fork) {
-    if (err == hipSuccess) err = hipEventRecord(c.join_ev, c.side_stream);
-    if (err == hipSuccess) err = hipStreamWaitEvent(st, c.join_ev, 0);
-    reassemble(3);
-  } else {
-    for (int i = 0; i < 4; ++i) reassemble(i);
-  }
+  for (int i = 0; i < 4; ++i) reassemble(i);
   // ---- fusion (refinenet4 .. refinenet1) ----
   dav2_fusion(4, b.rn[3], nullptr, B, hs[3], ws[3], b.p4, hs[2], ws[2]);
   dav2_fusion(3, b.p4, b.rn[2], B, hs[2], ws[2], b.p3, hs[1], ws[1]);
@@ -820,9 +767,6 @@ int mde_context_create(mde_engine* e, int max_batch, mde_context** out) {
   // zero once: the q/k/v^T pad rows/columns beyond T must stay 0
   he = hipMemset(c->arena, 0, c->arena_bytes);
   if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->cap_stream, hipStreamNonBlocking);
-  if (he == hipSuccess) he = hipStreamCreateWithFlags(&c->side_stream, hipStreamNonBlocking);
-  for (int i = 0; i < 3 && he == hipSuccess; ++i) he = hipEventCreateWithFlags(&c->fork_ev[i], hipEventDisableTiming);
-  if (he == hipSuccess) he = hipEventCreateWithFlags(&c->join_ev, hipEventDisableTiming);
   if (he == hipSuccess) he = hipDeviceSynchronize();
   if (he != hipSuccess) {
     hipFree(c->arena);
@@ -846,10 +790,6 @@ int mde_context_destroy(mde_context* c) {
     hipEventDestroy(pe.second.second);
   }
   if (c->cap_stream) hipStreamDestroy(c->cap_stream);
-  if (c->side_stream) hipStreamDestroy(c->side_stream);
-  for (hipEvent_t ev : c->fork_ev)
-    if (ev) hipEventDestroy(ev);
-  if (c->join_ev) hipEventDestroy(c->join_ev);
   if (c->arena) hipFree(c->arena);
   delete c;
   return MDE_OK;
@@ -950,7 +890,12 @@ int mde_context_enqueue(mde_context* c, void* stream) {
     }
     return MDE_OK;
   }
-  if (!c->graph_mode) {
+  // a caller capturing its own stream (its own hipGraph / torch.cuda.graph)
+  // gets the forward's kernels captured straight into that graph: no graph of
+  // ours is launched inside the capture, and none has to outlive it
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  HIP_OR(hipStreamIsCapturing(st, &cap), "hipStreamIsCapturing");
+  if (!c->graph_mode || cap != hipStreamCaptureStatusNone) {
     Runner r{*c, st, false};
     hipError_t he = run_forward(r, c->batch, in, out, out2);
     if (he != hipSuccess) return hip_fail(he, "enqueue");

@@ -15,6 +15,7 @@
 #include "../../include/mde.h"
 #include "mde_ops.h"
 #include "pack_format.h"
+#include "tuning.h"
 
 namespace mde {
 
@@ -39,9 +40,6 @@ struct DAV2Buf {
   size_t aws_bytes;
   float* st;        // folded-LN partials [B*T][D/32][2] (f16 residual + folded pack, else null)
   float* sws;       // E_STORE split-K partials (GemmParams::partial_cap = kSplitWsFloats)
-  float* sws2;      // the same for the reassemble branch forked onto the side stream
-  float* skws;      // stream-K partial tiles (GemmParams::sk_ws; small-batch contexts only, else null)
-  int* skcnt;       // stream-K tile arrival counters (zeroed with the arena)
 };
 
 // fp32 elements of a context's E_STORE split-K workspace (launch_gemm bounds
@@ -143,12 +141,6 @@ struct mde_context {
   mde::VGBuf v{};
   bool graph_mode = true;
   hipStream_t cap_stream = nullptr;
-  // DPT reassemble branch of taps 0..2 forked off the encoder (small grids):
-  // a second stream + fork / join events (captured into the graph as a
-  // parallel branch)
-  hipStream_t side_stream = nullptr;
-  hipEvent_t fork_ev[3] = {nullptr, nullptr, nullptr};
-  hipEvent_t join_ev = nullptr;
   // captured forwards per (batch, io addresses), at most kMaxGraphs of them:
   // the least recently launched one is destroyed to make room (a caller that
   // rebinds fresh buffers every call pays a capture, not unbounded growth)
@@ -278,19 +270,12 @@ struct Runner {
 
   // E_STORE split-K workspace for launch_gemm's small-grid policy (null: never split)
   float* split_ws = nullptr;
-  // stream-K workspace of the main stream (null: never stream-K)
-  float* sk_ws = nullptr;
-  int* sk_cnt = nullptr;
 
   void gemm(const char* name, const GemmParams& g) {
     GemmParams q = g;
     if (split_ws && g.emode == E_STORE && !g.partial) {
       q.partial = split_ws;
       q.partial_cap = kSplitWsFloats;
-    }
-    if (!q.sk_ws) {
-      q.sk_ws = sk_ws;
-      q.sk_cnt = sk_cnt;
     }
     step(name, [&] { return launch_gemm(q, st); });
   }

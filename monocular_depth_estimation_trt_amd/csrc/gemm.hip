@@ -35,6 +35,7 @@
 #include "mde_device.h"
 #include "mde_ops.h"
 #include "tile_epilogue.h"
+#include "tuning.h"
 
 #ifndef MDE_GEMM_BK
 #define MDE_GEMM_BK 64
@@ -389,8 +390,8 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
           }
           m2 += __shfl_xor(m2, 16);
           m2 += __shfl_xor(m2, 32);
-          // (RPW 8, 16-wave tiles: lanes 8..15 repeat the next wave's rows)
-          if ((lane >> 4) == 0 && (RPW >= 16 || (lane & 15) < RPW))
+          // only this wave's rows (RPW 8: lanes 8..15 hold the next wave's)
+          if ((lane >> 4) == 0 && g * 16 + (lane & 15) < RPW)
             *reinterpret_cast<float2*>(smem + SG * STAGE + r * 8) = make_float2(mean, m2 * invd);
         }
       }
@@ -477,265 +478,6 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
   if (!staged) store_tile<EM, TM, TN>(p, acc, mrow, n0 + wn * TN * 16 + (lane >> 4) * 4, lane, slice);
 }
 
-// ---- stream-K for batch-1 grids (dense A; E_STORE / E_QKV / E_RESID) ----
-// A 128^2-tile grid of a batch-1 ViT-L linear holds 264 (qkv) or 352 (fc1)
-// tiles for 256 CUs, or 88 long-K tiles (fc2): whole tiles per workgroup
-// leave a second round on some CUs or most of the chip idle.  Here one
-// workgroup per CU (128 KB ring) first takes `rounds` whole tiles, then the
-// first `gsk` workgroups take equal shares of the remaining (tile, K-step)
-// iterations, tile-major (>= 4 K-steps each).  A tile cut between workgroups
-// is finished by whichever of its contributors arrives last: each contributor
-// writes its fp32 accumulators to its own workspace slot, bumps the tile's
-// arrival counter, and the last one sums the slots in contributor order (a
-// fixed order: the result does not depend on arrival order), re-zeroes the
-// counter and runs the tile's epilogue.  No workgroup ever waits on another.
-// The slots and counters are accessed with system-scope (sc0 sc1) loads,
-// stores and atomics, which bypass the per-XCD L2s, so no cache-wide
-// write-back / invalidate is needed (a __threadfence() per contributor
-// measured 4x slower still).  Opt-in: see sk_eligible.
-struct SkArgs {
-  unsigned long long* ws;  // [2 * gridDim.x][TM * TN][512][2] fp32 pairs (a workgroup's first / last segment)
-  int* cnt;                // per-tile arrival counters (zero between launches)
-  long long total;         // tiles * ipt
-  int ipt;                 // K-steps per tile
-  int rounds;              // whole tiles per workgroup before the stream-K region
-  int gsk;                 // workgroups sharing the stream-K region
-};
-constexpr int kSkSlotU64 = 8 * 512 * 2;  // 8-byte words per slot (128^2 fp32)
-
-MDE_DEV unsigned long long f2_bits(float a, float b) {
-  return (unsigned long long)__float_as_uint(a) | ((unsigned long long)__float_as_uint(b) << 32);
-}
-
-template <int EM, int SG>
-__global__ void __launch_bounds__(512) gemm_sk_kernel(const GemmParams p, const SkArgs sk) {
-  constexpr int BM = 128, BN = 128, BK = 64, WN = 4, NW = 8, NT = 512, TM = 4, TN = 2;
-  static_assert(SG >= 2 && SG <= 4, "ring");
-  using G = KGeo<BK>;
-  constexpr int ROWB = G::ROWB, CH = G::CH;
-  constexpr int APASS = BM / G::RW / NW, BPASS = BN / G::RW / NW;  // 2, 2
-  constexpr int NPER = APASS + BPASS;
-  constexpr int STAGE = (BM + BN) * ROWB;  // 32 KB
-  constexpr bool LNF = EM == E_QKV || EM == E_STORE;
-  static_assert(TM * 16 * 2 == BM && TN * 16 * WN == BN && APASS * NW * G::RW == BM, "tile");
-  __shared__ __attribute__((aligned(16))) char smem[SG * STAGE + BM * 8];
-  __shared__ int s_last;
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave - (wave / WN) * WN;
-  const int nwg = gridDim.x;
-  // consecutive shares on one XCD: its L2 then holds the row blocks they share
-  const int v = MDE_XCD_REMAP ? xcd_remap(blockIdx.x, nwg) : blockIdx.x;
-  const long long base = (long long)sk.rounds * nwg * sk.ipt, rem = sk.total - base;
-  const int gsk = sk.gsk;
-  auto start = [&](int u) { return base + (long long)u * rem / gsk; };
-  // the workgroup whose stream-K share holds iteration x
-  auto owner = [&](long long x) { return (int)(((x - base + 1) * gsk + rem - 1) / rem - 1); };
-  const int ntn = (p.N + BN - 1) / BN;
-  const int lrow = lane / CH;
-  const int lch = G::pch(lrow, lane % CH);
-  auto aslot = [&](int i) { return (wave + i * NW) * G::RW * ROWB; };
-  long long it = v < gsk ? start(v) : 0;
-  const long long it1 = v < gsk ? start(v + 1) : 0;
-  for (int r = 0;; ++r) {
-    int tile, kt0, nk;
-    if (r < sk.rounds) {
-      tile = r * nwg + v;
-      kt0 = 0;
-      nk = sk.ipt;
-    } else {
-      if (it >= it1) break;
-      tile = (int)(it / sk.ipt);
-      kt0 = (int)(it - (long long)tile * sk.ipt);
-      nk = (int)min((long long)(sk.ipt - kt0), it1 - it);
-      it += nk;
-    }
-    const int tm = tile / ntn, tn = tile - (tile / ntn) * ntn;
-    const int m0 = tm * BM, n0 = tn * BN;
-
-    const f16* arow[APASS];
-#pragma unroll
-    for (int i = 0; i < APASS; ++i) {
-      const int gm = m0 + (wave + i * NW) * G::RW + lrow;
-      arow[i] = reinterpret_cast<const f16*>(p.A) + (size_t)(gm < p.M ? gm : p.M - 1) * p.lda;
-    }
-    const f16* wbase = reinterpret_cast<const f16*>(p.W) + (size_t)(n0 + wave * G::RW + lrow) * p.ldw + lch * 8;
-    auto issue = [&](int kt, int buf) {
-      char* sbase = smem + buf * STAGE;
-      const int k0 = (kt + kt0) * BK;
-#pragma unroll
-      for (int i = 0; i < BPASS; ++i) glds16(wbase + (size_t)i * NW * G::RW * p.ldw + k0, sbase + BM * ROWB + aslot(i));
-      const int k = k0 + lch * 8;
-      const int kk = k < p.K ? k : 0;
-#pragma unroll
-      for (int i = 0; i < APASS; ++i) glds16(arow[i] + kk, sbase + aslot(i));
-    };
-    f32x4 acc[TM][TN];
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    auto mma_stage = [&](int cur) {
-      const char* sA = smem + cur * STAGE;
-      const char* sB = sA + BM * ROWB;
-#pragma unroll
-      for (int s = 0; s < BK / 32; ++s) {
-        f16x8 fa[TM], fb[TN];
-        const int lc = 4 * s + (lane >> 4);
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const int r = wm * TM * 16 + i * 16 + (lane & 15);
-          fa[i] = *reinterpret_cast<const f16x8*>(sA + r * ROWB + G::pch(r, lc) * 16);
-        }
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int r = wn * TN * 16 + j * 16 + (lane & 15);
-          fb[j] = *reinterpret_cast<const f16x8*>(sB + r * ROWB + G::pch(r, lc) * 16);
-        }
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);
-      }
-    };
-    // folded LayerNorm rows' (mean, var) -> LDS behind the ring (as gemm_kernel)
-    float4 c1v[TN];
-    if constexpr (LNF) {
-      if (p.lnst_in) {
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          const int n = n0 + wn * TN * 16 + j * 16 + (lane >> 4) * 4;
-          c1v[j] = *reinterpret_cast<const float4*>(p.lnc1 + (n < p.N ? n : 0));
-        }
-      }
-    }
-#pragma unroll
-    for (int s = 0; s < SG - 1; ++s)
-      if (s < nk) issue(s, s);
-    if constexpr (LNF) {
-      if (p.lnst_in) {
-        const float2* st2 = reinterpret_cast<const float2*>(p.lnst_in);
-        const float invd = 1.f / (float)(p.lnst_ns * 32);
-        const int kp = p.lnst_ns >> 2;
-        const int r = wave * 16 + (lane & 15);  // BM / NW = 16 rows per wave
-        const int m = m0 + r;
-        const int mr = m < p.M ? m : p.M - 1;
-        float2 t[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) t[k] = st2[(size_t)((lane >> 4) + (k < kp ? 4 * k : 0)) * p.lnst_rows + mr];
-        float s1 = 0.f;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) s1 += k < kp ? t[k].x : 0.f;
-        s1 += __shfl_xor(s1, 16);
-        s1 += __shfl_xor(s1, 32);
-        const float mean = s1 * invd;
-        float m2 = 0.f;
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float d = t[k].x * (1.f / 32.f) - mean;
-          m2 += k < kp ? t[k].y + 32.f * d * d : 0.f;
-        }
-        m2 += __shfl_xor(m2, 16);
-        m2 += __shfl_xor(m2, 32);
-        if ((lane >> 4) == 0) *reinterpret_cast<float2*>(smem + SG * STAGE + r * 8) = make_float2(mean, m2 * invd);
-      }
-    }
-    for (int kt = 0; kt < nk; ++kt) {
-      const int after = min(nk - 1 - kt, SG - 2);
-      if (after >= 2) wait_vm_n<2 * NPER>();
-      else if (after == 1) wait_vm_n<NPER>();
-      else wait_vm_n<0>();
-      lds_barrier();
-      if (kt + SG - 1 < nk) issue(kt + SG - 1, (kt + SG - 1) % SG);
-      mma_stage(kt % SG);
-    }
-
-    if (kt0 != 0 || nk != sk.ipt) {
-      // a cut tile: publish this segment, the last contributor finishes it
-      const long long tb = (long long)tile * sk.ipt;
-      const int vf = owner(tb), vl = owner(tb + sk.ipt - 1);
-      auto slot = [&](int u) { return sk.ws + (size_t)(2 * u + (start(u) / sk.ipt == tile ? 0 : 1)) * kSkSlotU64; };
-      unsigned long long* mine = slot(v);
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) {
-          unsigned long long* d = mine + (size_t)((i * TN + j) * NT + tid) * 2;
-          __hip_atomic_store(d, f2_bits(acc[i][j][0], acc[i][j][1]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-          __hip_atomic_store(d + 1, f2_bits(acc[i][j][2], acc[i][j][3]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-        }
-      wait_vm();  // this wave's slot stores have completed
-      __syncthreads();
-      if (tid == 0)
-        s_last = __hip_atomic_fetch_add(sk.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) == vl - vf;
-      __syncthreads();
-      if (!s_last) continue;  // every wave is past its LDS reads: the next segment may refill the ring
-      f32x4 sum[TM][TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) sum[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int u = vf; u <= vl; ++u) {
-        unsigned long long* src = slot(u);
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            f32x4 a = acc[i][j];
-            if (u != v) {
-              unsigned long long* q = src + (size_t)((i * TN + j) * NT + tid) * 2;
-              const unsigned long long lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              const unsigned long long hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-              a = f32x4{__uint_as_float((unsigned)lo), __uint_as_float((unsigned)(lo >> 32)),
-                        __uint_as_float((unsigned)hi), __uint_as_float((unsigned)(hi >> 32))};
-            }
-            sum[i][j] += a;
-          }
-      }
-#pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j) acc[i][j] = sum[i][j];
-      if (tid == 0) __hip_atomic_store(sk.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-    }
-
-    if constexpr (LNF) {
-      if (p.lnst_in) {
-#pragma unroll
-        for (int i = 0; i < TM; ++i) {
-          const float2 mv = *reinterpret_cast<const float2*>(smem + SG * STAGE + (wm * TM * 16 + i * 16 + (lane & 15)) * 8);
-          const float rstd = rsqrtf(mv.y + p.ln_eps);
-          const float nm = -rstd * mv.x;
-#pragma unroll
-          for (int j = 0; j < TN; ++j) {
-            const float4 c = c1v[j];
-            acc[i][j][0] = fmaf(rstd, acc[i][j][0], nm * c.x);
-            acc[i][j][1] = fmaf(rstd, acc[i][j][1], nm * c.y);
-            acc[i][j][2] = fmaf(rstd, acc[i][j][2], nm * c.z);
-            acc[i][j][3] = fmaf(rstd, acc[i][j][3], nm * c.w);
-          }
-        }
-      }
-    }
-    int mrow[TM];
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = m0 + wm * TM * 16 + i * 16 + (lane & 15);
-      mrow[i] = m < p.M ? m : -1;
-    }
-    lds_barrier();  // the ring's last stage may still be read by other waves
-    const int m0w = m0 + wm * TM * 16;
-    bool staged = false;
-    if constexpr (MDE_EPI_LDS)
-      staged = store_tile_lds<EM, TM, TN, 0>(
-          p, acc, [&](int row) { return m0w + row < p.M ? m0w + row : -1; }, n0 + wn * TN * 16, lane,
-          smem + wave * (TM * 16) * (TN * 16) * 4);
-    if (!staged) store_tile<EM, TM, TN>(p, acc, mrow, n0 + wn * TN * 16 + (lane >> 4) * 4, lane);
-    __syncthreads();  // staging reads done before the next segment refills the ring
-  }
-}
-
 template <int BM, int BN, int WM, int WN, int AM, int EM, int BKSEL = MDE_GEMM_BK, int STG = 0>
 hipError_t run(const GemmParams& p, hipStream_t st) {
   const int gm = (p.M + BM - 1) / BM, gn = (p.N + BN - 1) / BN;
@@ -746,110 +488,26 @@ hipError_t run(const GemmParams& p, hipStream_t st) {
   return hipGetLastError();
 }
 
-// dense 128^2 tiles on the BK 32 / 3-stage / three-per-CU kernel
-// (MDE_GEMM_BK32=0: the BK 64 two-stage kernel, A/B)
-int bk32_kmax() {  // MDE_GEMM_BK32_KMAX: tuning
-  static const int v = [] {
-    const char* e = getenv("MDE_GEMM_BK32_KMAX");
-    return e ? atoi(e) : 768;
-  }();
-  return v;
-}
-bool bk32_tiles() {
-  static const int v = [] {
-    const char* e = getenv("MDE_GEMM_BK32");
-    return (e && e[0] == '0') ? 0 : 1;
-  }();
-  return v != 0;
-}
-
-// tuning override for large dense problems: MDE_GEMM_TILE = 256x256 | 256x128 | 128x256
-// (read per launch: tests toggle it; a captured graph keeps its choice)
-int tile_override() {
-  {
-    const char* e = getenv("MDE_GEMM_TILE");
-    if (!e) return 0;
-    if (!strcmp(e, "256x256")) return 1;
-    if (!strcmp(e, "256x128")) return 2;
-    if (!strcmp(e, "128x256")) return 3;
-    if (!strcmp(e, "256x128w8")) return 4;  // 8 waves, BK 32 x 3 stages, two workgroups per CU
-    if (!strcmp(e, "128x128w8")) return 5;  // 8 waves (2 x 4 of 64 x 32) on the 128^2 tile, any grid
-    if (!strcmp(e, "big1")) return 6;       // small grids: tall tiles, 3-deep ring, one workgroup per CU
-    if (!strcmp(e, "64x128w8")) return 7;   // small grids: 64 x 128 tiles, 8 waves, three workgroups per CU
-    return 0;
-  }
-}
+// dense short-K stores (K <= 768) take the BK 32 / 3-stage / three-per-CU
+// 128^2 kernel; 128^2 tiles once the grid holds at least kBigTileMin of them
+constexpr int kBk32Kmax = 768;
+constexpr long long kBigTileMin = 240;
 
 // 64^2 tiles of a grid that fits two workgroups per CU run a 4-deep ring (64
 // KB: 48 KB of K-steps in flight instead of 16): the batch-1 linears and
-// split-K slices are latency-bound on their one K-step in flight.
-// MDE_GEMM_DEEP64=0 turns it off (read per launch).
-bool deep64(long long wgs) {
-  const char* e = getenv("MDE_GEMM_DEEP64");
-  if (e && e[0] == '0') return false;
-  return wgs <= 512;
-}
+// split-K slices are latency-bound on their one K-step in flight.  Switch
+// "deep64" (tuning.h).
+bool deep64(long long wgs) { return knob(KNOB_DEEP64) && wgs <= 512; }
 
 // 128^2 tiles of a grid under two workgroups per CU run 8 waves (2 x 4 of 64
 // x 32): a lone workgroup per CU otherwise has one wave per SIMD to cover its
 // own LDS reads and barrier waits.  ViT-L B=1 fc1 0.665 -> 0.635, fc2 (split
 // slices) 0.830 -> 0.809 ms per forward (profiles/r03_v4_bench_vitl1w8).
-// MDE_GEMM_W8SMALL=0 turns it off (read per launch).
-bool w8small(long long wgs) {
-  const char* e = getenv("MDE_GEMM_W8SMALL");
-  if (e && e[0] == '0') return false;
-  return wgs < 512;
-}
-
-// MDE_GEMM_W16=1: 16 waves (4 x 4 of 32 x 32) on those small-grid 128^2
-// tiles instead of 8 (tuning; read per launch)
-bool w16small() {
-  const char* e = getenv("MDE_GEMM_W16");
-  return e && e[0] == '1';
-}
-
-// 128^2 tiles once the grid holds at least this many of them (MDE_GEMM_BIG_MIN: tuning)
-long long big_tile_min() {
-  static const long long v = [] {
-    const char* e = getenv("MDE_GEMM_BIG_MIN");
-    return e ? atoll(e) : 240ll;
-  }();
-  return v;
-}
+// Switch "w8small".
+bool w8small(long long wgs) { return knob(KNOB_W8SMALL) && wgs < 512; }
 
 template <int AM, int EM>
 hipError_t dispatch(const GemmParams& p, hipStream_t st) {
-  if constexpr (AM == A_DENSE && EM != E_HEAD) {
-    const long long t256 = (long long)((p.M + 255) / 256) * ((p.N + 255) / 256);
-    if (t256 >= 512) {
-      switch (tile_override()) {
-        case 1: return run<256, 256, 2, 2, AM, EM>(p, st);
-        case 2: return run<256, 128, 2, 2, AM, EM>(p, st);
-        case 3: return run<128, 256, 2, 2, AM, EM>(p, st);
-        default: break;
-      }
-    }
-  }
-  if constexpr (AM == A_DENSE && EM != E_HEAD) {
-    // 256 x 128 tiles on 8 waves (4 x 2 of 64 x 64), BK 32 x 3 stages = 72 KB:
-    // two workgroups per CU, 25 % fewer L2 -> LDS bytes per FLOP than 128^2
-    if (tile_override() == 4 && p.M >= 256 && p.N >= 128) return run<256, 128, 4, 2, AM, EM, 32>(p, st);
-    if (tile_override() == 5 && p.N >= 128) return run<128, 128, 2, 4, AM, EM>(p, st);
-    if constexpr (EM == E_STORE || EM == E_QKV) {
-      // small grids (under one 128^2 tile per CU... up to ~1.4): the tallest
-      // row block that keeps the grid within one workgroup per CU, on a
-      // 3-deep ring (2 K-steps, 72-80 KB, in flight per CU)
-      if (tile_override() == 6 && p.N >= 128 && !p.lnst_out) {
-        const long long gn = (p.N + 127) / 128;
-        const long long t128 = (long long)((p.M + 127) / 128) * gn;
-        if (t128 < 512) {
-          if (t128 <= 256) return run<128, 128, 2, 2, AM, EM, 64, 3>(p, st);
-          if ((long long)((p.M + 159) / 160) * gn <= 256) return run<160, 128, 2, 2, AM, EM, 64, 3>(p, st);
-          if ((long long)((p.M + 191) / 192) * gn <= 256) return run<192, 128, 2, 2, AM, EM, 64, 3>(p, st);
-        }
-      }
-    }
-  }
   if constexpr (EM == E_HEAD) {
     return run<128, 32, 4, 1, AM, EM>(p, st);
   } else {
@@ -867,24 +525,16 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
       // FLOP and twice the rows per workgroup for the read-modify-write
       // epilogue.  ViT-S B = 48, same box, two passes: proj 0.685 / 0.690 ->
       // 0.611 / 0.606 ms, fc2 1.493 / 1.503 -> 1.401 / 1.394 ms per forward,
-      // qkv / fc1 unchanged on this tile (profiles/r03_v3_*).  MDE_RESID_W8=0: off
-      static const bool w8 = [] {
-        const char* e = getenv("MDE_RESID_W8");
-        return !(e && e[0] == '0');
-      }();
+      // qkv / fc1 unchanged on this tile (profiles/r03_v3_*)
       const long long t256 = (long long)((p.M + 255) / 256) * ((p.N + 127) / 128);
-      if (w8 && t256 >= 512) return run<256, 128, 4, 2, AM, EM, 32>(p, st);
+      if (t256 >= 512) return run<256, 128, 4, 2, AM, EM, 32>(p, st);
       // short-K residual updates (ViT-S proj, K 384) on 128 x 64 tiles: 48 KB
       // LDS with full fp32 staging, three workgroups per CU (B=28: proj
       // 0.427/0.431 -> 0.419/0.425 ms per forward, two same-box runs; fc2 at
-      // K 1536 loses, 0.86 -> 0.97).  MDE_RESID_N64_KMAX overrides the bound.
-      static const int kmax = [] {
-        const char* e = getenv("MDE_RESID_N64_KMAX");
-        return e ? atoi(e) : 384;
-      }();
-      if (p.K <= kmax && big >= big_tile_min()) return run<128, 64, 4, 1, AM, EM>(p, st);
+      // K 1536 loses, 0.86 -> 0.97)
+      if (p.K <= 384 && big >= kBigTileMin) return run<128, 64, 4, 1, AM, EM>(p, st);
     }
-    if (big >= big_tile_min()) {
+    if (big >= kBigTileMin) {
       // short-K stores (ViT-S/B qkv, fc1: K 384 / 768 -> 6-12 K-steps, the
       // epilogue a third of the launch) gain from the third workgroup per CU
       // (B=28 ViT-S: fc1 1.30 -> 1.10 ms, qkv 0.97 -> 0.89 per forward); the
@@ -892,9 +542,7 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
       // staging passes, proj 0.43 -> 0.45 even with f16 staging of the
       // update; ViT-L B=8 qkv 2.56 -> 2.67)
       if constexpr (AM == A_DENSE && (EM == E_STORE || EM == E_QKV)) {
-        if (p.K <= bk32_kmax() && bk32_tiles()) return run<128, 128, 2, 2, AM, EM, 32>(p, st);
-        if (tile_override() == 7 && w8small(big)) return run<64, 128, 2, 4, AM, EM>(p, st);
-        if (w16small() && w8small(big)) return run<128, 128, 4, 4, AM, EM>(p, st);
+        if (p.K <= kBk32Kmax) return run<128, 128, 2, 2, AM, EM, 32>(p, st);
         if (w8small(big)) return run<128, 128, 2, 4, AM, EM>(p, st);
       }
       return run<128, 128, 2, 2, AM, EM>(p, st);
@@ -907,15 +555,6 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
     }
     return run<64, 64, 2, 2, AM, EM>(p, st);
   }
-}
-
-// MDE_CONV_IM2COL=1 forces the implicit-im2col GEMM path for 3x3 convs (A/B aid).
-bool getenv_im2col() {
-  static const int v = [] {
-    const char* e = getenv("MDE_CONV_IM2COL");
-    return (e && e[0] == '1') ? 1 : 0;
-  }();
-  return v != 0;
 }
 
 // Direct-conv tiles are 8 x 16 output pixels per image: on small maps most of
@@ -941,8 +580,7 @@ int store_split_slices(const GemmParams& p) {
   if (p.emode != E_STORE || !p.partial || p.partial_cap == 0 || p.lnst_in || p.lnst_out) return 1;
   if (p.amode != A_DENSE && p.amode != A_CONV3) return 1;
   if (p.amode == A_CONV3 && p.stride != 1 && p.stride != 2) return 1;
-  const char* off = getenv("MDE_SPLITK");  // read per call: tests toggle it (captured graphs keep their choice)
-  if (off && off[0] == '0') return 1;
+  if (!knob(KNOB_SPLITK)) return 1;
   const int nk = (p.K + 63) / 64;
   const long long t64 = (long long)((p.M + 63) / 64) * ((p.N + 63) / 64);
   // workgroups of the unsplit launch
@@ -952,20 +590,16 @@ int store_split_slices(const GemmParams& p) {
     wgs = (long long)p.cb * ((p.oh + 7) / 8) * ((p.ow + 15) / 16) * ((p.N + bn - 1) / bn);
   } else {
     const long long big = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128);
-    wgs = big >= big_tile_min() ? big : t64;
+    wgs = big >= kBigTileMin ? big : t64;
   }
   // at least 12 K-steps: the 64-channel convs of the ViT-S DPT (K 576, 9
   // steps) run better unsplit (ViT-S B=1 0.925 -> 0.902 ms per forward with
-  // 12 vs 8; 16: 0.909); MDE_SPLIT_NKMIN overrides
-  static const int nkmin = [] {
-    const char* e = getenv("MDE_SPLIT_NKMIN");
-    return e ? atoi(e) : 12;
-  }();
-  if (wgs >= 256 || nk < nkmin) return 1;
+  // 12 vs 8; 16: 0.909)
+  if (wgs >= 256 || nk < 12) return 1;
   // fill two workgroups per CU without spilling into a third: the slices then
   // run the 4-deep ring (deep64), which a 513th workgroup would forfeit
   int S = (int)((512 + t64 - 1) / t64);
-  if (deep64(1) && 512 / t64 >= 2) S = (int)(512 / t64);
+  if (512 / t64 >= 2) S = (int)(512 / t64);  // (independent of the "deep64" switch: same slices either way)
   S = S < nk / 4 ? S : nk / 4;  // >= 4 K-steps per slice
   S = S < 16 ? S : 16;
   while (S > 1 && (size_t)S * p.M * p.N > p.partial_cap) --S;
@@ -1003,79 +637,6 @@ bool lnst_valid(const GemmParams& p) {
            (p.lnst_in && (!p.lnc1 || p.amode != A_DENSE)) || (p.lnst_out && !p.xh));
 }
 
-// stream-K (gemm_sk_kernel) for a dense E_STORE / E_QKV / E_RESID problem
-// whose 128^2 grid is not a whole number of rounds over the CUs and is under
-// two of them, with >= MDE_GEMM_SK_MIN (12) K-steps per workgroup.  Opt-in
-// (MDE_GEMM_SK=1, read per launch): measured slower than the whole-tile
-// kernels at ViT-L B=1 (3.20 -> 4.33 ms per forward at one workgroup per CU,
-// 5.55 at two), see DESIGN.md.
-int sk_workgroups() {
-  static const int v = [] {
-    int d = 0, n = 0;
-    if (hipGetDevice(&d) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess)
-      n = kSkMaxWG;
-    return n < 1 ? 1 : (n > kSkMaxWG ? kSkMaxWG : n);
-  }();
-  return v;
-}
-bool sk_eligible(const GemmParams& p) {
-  if (!p.sk_ws || !p.sk_cnt || p.amode != A_DENSE || p.a_tok > 1) return false;
-  if (p.emode != E_STORE && p.emode != E_QKV && p.emode != E_RESID) return false;
-  const char* e = getenv("MDE_GEMM_SK");  // default off (measured slower)
-  if (!(e && e[0] == '1')) return false;
-  static const int kmin = [] {
-    const char* s = getenv("MDE_GEMM_SK_MIN");
-    return s ? atoi(s) : 12;
-  }();
-  const long long tiles = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128);
-  const int G = sk_workgroups();
-  if (tiles > kSkMaxTiles || tiles >= 2ll * G || tiles % G == 0) return false;
-  return tiles * ((p.K + 63) / 64) >= (long long)kmin * G;
-}
-// MDE_GEMM_SK_OCC: stream-K workgroups per CU -- 1 (default): four-stage
-// ring, 129 KB; 2: two-stage ring, 65 KB
-int sk_occ() {
-  static const int v = [] {
-    const char* s = getenv("MDE_GEMM_SK_OCC");
-    return (s && s[0] == '2') ? 2 : 1;
-  }();
-  return v;
-}
-hipError_t launch_sk(const GemmParams& p, hipStream_t st) {
-  static const int minpiece = [] {  // MDE_GEMM_SK_PIECE: least K-steps per stream-K share
-    const char* s = getenv("MDE_GEMM_SK_PIECE");
-    const int v = s ? atoi(s) : 4;
-    return v < 1 ? 1 : v;
-  }();
-  const int occ = sk_occ();
-  const int G = sk_workgroups() * occ;  // workgroup slots (<= 2 * kSkMaxWG: the workspace holds 2 slots each)
-  const long long tiles = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128);
-  SkArgs a;
-  a.ws = reinterpret_cast<unsigned long long*>(p.sk_ws);
-  a.cnt = p.sk_cnt;
-  a.ipt = (p.K + 63) / 64;
-  a.total = tiles * a.ipt;
-  a.rounds = (int)(tiles / G);
-  const long long rem = a.total - (long long)a.rounds * G * a.ipt;  // > 0: tiles % G != 0
-  const long long g = rem / minpiece;
-  a.gsk = (int)(g < 1 ? 1 : (g > G ? G : g));
-  const dim3 grid((unsigned)G), blk(512);
-  if (occ == 1) {
-    switch (p.emode) {
-      case E_STORE: hipLaunchKernelGGL((gemm_sk_kernel<E_STORE, 4>), grid, blk, 0, st, p, a); break;
-      case E_QKV: hipLaunchKernelGGL((gemm_sk_kernel<E_QKV, 4>), grid, blk, 0, st, p, a); break;
-      default: hipLaunchKernelGGL((gemm_sk_kernel<E_RESID, 4>), grid, blk, 0, st, p, a); break;
-    }
-  } else {
-    switch (p.emode) {
-      case E_STORE: hipLaunchKernelGGL((gemm_sk_kernel<E_STORE, 2>), grid, blk, 0, st, p, a); break;
-      case E_QKV: hipLaunchKernelGGL((gemm_sk_kernel<E_QKV, 2>), grid, blk, 0, st, p, a); break;
-      default: hipLaunchKernelGGL((gemm_sk_kernel<E_RESID, 2>), grid, blk, 0, st, p, a); break;
-    }
-  }
-  return hipGetLastError();
-}
-
 }  // namespace
 
 int gemm_store_split_slices(const GemmParams& p) { return store_split_slices(p); }
@@ -1095,16 +656,11 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
   if (p.emode == E_CONVT && ((p.cout & 7) || (p.ldo & 7) || p.ldo < p.cout || ((uintptr_t)p.out16 & 15)))
     return hipErrorInvalidValue;
   if (p.emode == E_HEAD && (p.N != 32 || p.amode == A_DENSE)) return hipErrorInvalidValue;
-  if (sk_eligible(p)) {
-    if ((p.lnst_out || p.lnst_in) && !lnst_valid(p)) return hipErrorInvalidValue;
-    if ((p.emode == E_RESID && p.xh && ((uintptr_t)p.xh & 15)) || ((uintptr_t)p.sk_ws & 7)) return hipErrorInvalidValue;
-    return launch_sk(p, st);
-  }
   if (const int S = store_split_slices(p); S > 1) {
     if ((p.ldo & 7) || ((uintptr_t)p.partial & 15)) return hipErrorInvalidValue;
     return p.amode == A_DENSE ? launch_split_store<A_DENSE>(p, S, st) : launch_split_store<A_CONV3>(p, S, st);
   }
-  if (p.amode != A_DENSE && conv_direct_supported(p) && !getenv_im2col() && !prefer_im2col(p))
+  if (p.amode != A_DENSE && conv_direct_supported(p) && !prefer_im2col(p))
     return launch_conv3(p, st);
   if ((p.emode == E_RESID || p.emode == E_PATCH) && p.xh && ((uintptr_t)p.xh & 15)) return hipErrorInvalidValue;
   if (p.emode == E_RESID && p.splitk > 1 && p.partial && p.amode == A_DENSE) {
@@ -1115,10 +671,9 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
     // FLOP of the 64^2 ones; `partial` holds 4 slices (engine contract)
     const int nk = (p.K + 63) / 64;
     const long long t128 = (long long)((p.M + 127) / 128) * ((p.N + 127) / 128);
-    const char* e128 = getenv("MDE_SPLITK128");
-    const bool big = t128 * 4 >= 320 && nk >= 16 && !(e128 && e128[0] == '0');
+    const bool big = t128 * 4 >= 320 && nk >= 16;
     int S = big ? 4 : (p.splitk < nk ? p.splitk : nk);
-    if (!big && deep64(1)) {  // keep the 64^2 slices within two workgroups per CU (deep ring)
+    if (!big) {  // keep the 64^2 slices within two workgroups per CU (deep ring; same slices with "deep64" off)
       const long long t64 = (long long)((p.M + 63) / 64) * ((p.N + 63) / 64);
       while (S > 2 && t64 * S > 512) --S;
     }
@@ -1131,11 +686,7 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
     q.bias = nullptr;
     q.ls = nullptr;
     q.lnst_out = nullptr;  // the reduce kernel writes the LN partials
-    const long long t192 = (long long)((p.M + 191) / 192) * ((p.N + 127) / 128);
-    if (big && tile_override() == 6 && t192 * 4 <= 256) {
-      hipLaunchKernelGGL((gemm_kernel<192, 128, MDE_GEMM_BK, 2, 2, A_DENSE, E_PARTIAL, 3>),
-                         dim3((unsigned)t192, (unsigned)S), dim3(256), 0, st, q);
-    } else if (big && (tile_override() == 5 || w8small(t128 * S))) {
+    if (big && w8small(t128 * S)) {
       hipLaunchKernelGGL((gemm_kernel<128, 128, MDE_GEMM_BK, 2, 4, A_DENSE, E_PARTIAL>), dim3((unsigned)t128, (unsigned)S),
                          dim3(512), 0, st, q);
     } else if (big) {

@@ -32,6 +32,7 @@
 
 #include "mde_device.h"
 #include "mde_ops.h"
+#include "tuning.h"
 #include "tile_epilogue.h"
 
 #ifndef MDE_EPI_LDS_256
@@ -256,10 +257,7 @@ __global__ void __launch_bounds__(NW * 64) gemm256_kernel(const GemmParams p) {
 }  // namespace
 
 bool gemm256_eligible(const GemmParams& p) {
-  static const int mode = [] {
-    const char* e = getenv("MDE_GEMM256");  // 0: never, 1: auto (default), 2: always when legal
-    return e ? atoi(e) : 1;
-  }();
+  const int mode = knob(KNOB_GEMM256);  // 0: never, 1: auto (default), 2: always when legal
   if (mode == 0 || p.amode != A_DENSE || p.emode == E_HEAD) return false;
   if (p.M < 256 || p.N < 256) return false;
   // short K (ViT-S: 384): the prologue/epilogue of a one-workgroup-per-CU tile

@@ -88,15 +88,7 @@ struct GemmParams {
   // partial row) (m / (a_tok - 1)) * a_tok + 1 + m % (a_tok - 1), i.e. every
   // sequence's first (cls) row is skipped
   int a_tok = 0;
-  // stream-K workspace (batch-1 grids, gemm.hip gemm_sk_kernel): sk_ws =
-  // fp32 [2 * 2 * kSkMaxWG][128 * 128] partial tiles, sk_cnt = kSkMaxTiles int
-  // arrival counters, zero-initialised and left zero by every launch; null:
-  // never stream-K.  The workspace belongs to one stream at a time.
-  float* sk_ws = nullptr; int* sk_cnt = nullptr;
 };
-constexpr int kSkMaxWG = 256;
-constexpr int kSkMaxTiles = 4096;
-constexpr size_t kSkWsFloats = size_t(2) * 2 * kSkMaxWG * 128 * 128;  // two slots per workgroup, two workgroups per CU
 
 // x32[m*ldo+n] += ls[n] * (sum_{s<S} P[s][m][n] + bias[n]), slices summed in
 // order (elementwise.hip): the second half of the E_RESID split-K path
@@ -117,14 +109,15 @@ bool conv_direct_supported(const GemmParams& p);
 hipError_t launch_conv3(const GemmParams& p, hipStream_t st);
 
 // 256x256 phase-pipelined dense GEMM (gemm256.hip) for large token-major
-// problems; launch_gemm routes there when gemm256_eligible() (MDE_GEMM256=0 off).
+// problems; launch_gemm routes there when gemm256_eligible() (switch "gemm256").
 bool gemm256_eligible(const GemmParams& p);
 hipError_t launch_gemm256(const GemmParams& p, hipStream_t st);
 
 // ws (optional, attention_split_ws_bytes): fp32 workspace for the split-KV
 // path the launcher takes on grids too small to fill the chip (batch 1)
-// cfg (optional) = the MDE_ATTN_CFG syntax ("8", "4s2", "4g2", ...): forces a
-// workgroup shape / split for tests and tuning; nullptr = env, then the policy.
+// cfg (optional) = "<waves>[s<split>][g<groups>][r<ring>][q2]" ("8", "4s2",
+// "4g2", ...): forces a workgroup shape / split for tests and tuning; nullptr
+// or "" = the launch policy.
 hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T,
                             int Tpad, int ldo, hipStream_t st, float* ws = nullptr, size_t ws_bytes = 0,
                             const char* cfg = nullptr);

@@ -1,0 +1,43 @@
+// Process-wide dispatch switches of libmde_hip (internal).
+//
+// Every runtime switch of the library lives in one table (tuning.hip): each
+// entry starts at its default, is overridden ONCE per process from the
+// environment variable MDE_<NAME> (the only getenv site of the library), and
+// can be changed afterwards through the C ABI (mde_tuning_set / _get,
+// include/mde.h) -- the parity tests toggle them that way to compare a path
+// against its alternative.  A captured hipGraph keeps the choice it was
+// captured with.  Every switch has a GPU test that exercises both settings
+// (tests/test_gpu_*.py, named beside each entry below).
+#pragma once
+
+namespace mde {
+
+enum Knob : int {
+  // E_STORE / E_RESID split-K of small-grid GEMMs and DPT convs (1: on).
+  // test_fc2_splitk_matches_unsplit, test_conv3x3_splitk
+  KNOB_SPLITK = 0,
+  // LayerNorm folded into the consumer GEMMs of f16-residual engines (1: on;
+  // read at context creation).  test_lnfold_matches_layernorm
+  KNOB_LNFOLD,
+  // narrower direct-conv channel tiles on small grids (1: on).
+  // test_conv_narrow_tiles_bit_exact
+  KNOB_CONV_NARROW,
+  // separable upsampling conv for the 32-channel head convs (1: on).
+  // test_upconv_matches_conv3
+  KNOB_UPCONV,
+  // 256^2 phase-pipelined GEMM for large long-K problems (0 never, 1 auto, 2
+  // whenever legal).  test_gemm256_modes_match
+  KNOB_GEMM256,
+  // 4-deep LDS ring for small-grid 64^2 tiles (1: on).
+  // test_gemm_small_grid_variants_bit_exact
+  KNOB_DEEP64,
+  // 8 waves on small-grid 128^2 tiles (1: on).
+  // test_gemm_small_grid_variants_bit_exact
+  KNOB_W8SMALL,
+  KNOB_COUNT
+};
+
+// current value of a switch (relaxed atomic read; cheap enough per launch)
+int knob(Knob k);
+
+}  // namespace mde

@@ -243,8 +243,7 @@ void Runner::vggt_block(const std::string& p, float eps, bool qk, int seqs, int 
     // small batch: split fc2's K = 4D loop (as the DA-V2 fc2, engine.hip);
     // B = 1, S = 1: 352 64^2 tiles x 2 slices
     const long long t64 = (long long)((rows + 63) / 64) * ((D + 63) / 64);
-    const char* sk = getenv("MDE_SPLITK");
-    if (v.ws && (size_t)rows <= v.ws_rows && t64 < 512 && mlp >= 1024 && !(sk && sk[0] == '0')) {
+    if (v.ws && (size_t)rows <= v.ws_rows && t64 < 512 && mlp >= 1024 && knob(KNOB_SPLITK)) {
       g.partial = v.ws;
       g.splitk = t64 < 256 ? 4 : 2;
     }

@@ -71,6 +71,9 @@ class Engine:
         self._h = C.c_void_p(handle)
         self.device = device
         self.path = path
+        # torch imported after libmde_hip was loaded maps a second HIP runtime
+        # (_lib.check_single_runtime): refuse to run in that state
+        _lib.check_single_runtime()
         self._profile = tuple(tuple(int(v) for v in s) for s in profile) if profile else None
         self._static_batch = int(static_batch)
         self._contexts = weakref.WeakSet()

@@ -34,7 +34,8 @@ def test_header_declares_the_api():
 
 
 def test_every_declared_symbol_is_exported(lib_path):
-    lib = ctypes.CDLL(lib_path)
+    from monocular_depth_estimation_trt_amd import _lib
+    lib = _lib.lib()  # (a bare ctypes.CDLL before torch would map a second HIP runtime)
     missing = [f for f in declared_functions() if not hasattr(lib, f)]
     assert not missing, missing
 
@@ -69,3 +70,69 @@ def test_errors_without_gpu_are_reported_not_crashed(lib_path):
     assert rc == 3 and b"magic" in L.mde_last_error()
     rc = L.mde_op_linear(None, 8, None, 64, 4, 4, 8, None, 0, None, 4, None)
     assert rc == 1
+
+
+def test_tuning_switches(lib_path):
+    """The library's dispatch switches (include/mde.h mde_tuning_set/_get):
+    defaults, range and name checks, and the context manager restores."""
+    from monocular_depth_estimation_trt_amd import _lib
+    L = _lib.lib()
+    for name in _lib.TUNING:
+        assert _lib.get_tuning(name) == 1, name
+    v = ctypes.c_int()
+    assert L.mde_tuning_get(b"no_such_switch", ctypes.byref(v)) == 5
+    assert L.mde_tuning_set(b"splitk", 2) == 1
+    assert L.mde_tuning_set(b"gemm256", 2) == 0 and _lib.get_tuning("gemm256") == 2
+    _lib.set_tuning("gemm256", 1)
+    with _lib.tuning(splitk=0, deep64=0):
+        assert _lib.get_tuning("splitk") == 0 and _lib.get_tuning("deep64") == 0
+    assert _lib.get_tuning("splitk") == 1 and _lib.get_tuning("deep64") == 1
+    with pytest.raises(ValueError):
+        _lib.set_tuning("lnfold", 7)
+
+
+def _run_py(code, env=None):
+    import subprocess
+    import sys
+    e = dict(os.environ)
+    e.update(env or {})
+    r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, capture_output=True, text=True, timeout=600, env=e)
+    return r.returncode, r.stdout + r.stderr
+
+
+def test_tuning_reads_environment_once(lib_path):
+    rc, out = _run_py("from monocular_depth_estimation_trt_amd import _lib\n"
+                      "print(_lib.get_tuning('splitk'), _lib.get_tuning('gemm256'), _lib.get_tuning('w8small'))",
+                      {"MDE_SPLITK": "0", "MDE_GEMM256": "2", "MDE_GEMM_W8SMALL": "bogus"})
+    assert rc == 0, out
+    assert out.split()[-3:] == ["0", "2", "1"], out
+
+
+def test_one_hip_runtime_when_torch_comes_first(lib_path):
+    """_lib.lib() brings torch's bundled HIP runtime up first; libmde_hip then
+    binds to it (same SONAME), so exactly one runtime is mapped and it is
+    torch's -- the runtime that owns the streams torch passes in."""
+    rc, out = _run_py("from monocular_depth_estimation_trt_amd import _lib\n"
+                      "_lib.lib()\n"
+                      "print('RT', _lib.hip_runtimes())")
+    assert rc == 0, out
+    line = [l for l in out.splitlines() if l.startswith("RT ")][-1]
+    rts = eval(line[3:])
+    assert len(rts) == 1 and "torch" in rts[0], out
+
+
+def test_two_hip_runtimes_are_refused(lib_path):
+    """libmde_hip loaded before torch maps ROCm's runtime; a later torch
+    import maps its own second copy (the r3 smoke failure).  The binding
+    refuses that state with an explanation instead of failing in hipSetDevice."""
+    rc, out = _run_py("import ctypes\n"
+                      f"ctypes.CDLL({lib_path!r})\n"
+                      "import torch\n"
+                      "torch.cuda.is_available()\n"
+                      "from monocular_depth_estimation_trt_amd import _lib\n"
+                      "try:\n"
+                      "    _lib.lib()\n"
+                      "except ImportError as e:\n"
+                      "    print('REFUSED', e)\n")
+    assert rc == 0, out
+    assert "REFUSED two HIP runtimes" in out, out

@@ -28,7 +28,7 @@ import torch
 from conftest import GOLDEN
 from gpu_util import depth_metrics
 
-from monocular_depth_estimation_trt_amd import pack, weights
+from monocular_depth_estimation_trt_amd import _lib, pack, weights
 from monocular_depth_estimation_trt_amd.engine import Engine
 
 pytestmark = pytest.mark.gpu
@@ -173,20 +173,17 @@ def test_batch_and_graph_consistency(gpu):
 def test_fc2_splitk_matches_unsplit(gpu, encoder, size):
     """Small-batch contexts split fc2's K loop (gemm.hip launch_gemm: ViT-S at
     98^2 4 slices of 64^2 tiles, ViT-L at 518^2 4 slices of 128^2 tiles --
-    config 3's B=1); the slices are
-    summed in order, so the result is deterministic and equal to the unsplit
-    GEMM up to fp32 reassociation."""
+    config 3's B=1); the slices are summed in order, so the result is
+    deterministic and equal to the unsplit GEMM (switch "splitk" = 0) up to
+    fp32 reassociation."""
     cfg = weights.model_config(encoder, "metric")
     sd = weights.synthetic_state_dict(cfg, 5)
     blob = pack.pack_bytes(sd, cfg, size, size)
     x = weights.synthetic_images(1, size, size, first_seed=21)
     y_split = run_engine(blob, x, graph=True)
     assert np.array_equal(y_split, run_engine(blob, x, graph=False)), "split-K must be deterministic"
-    os.environ["MDE_SPLITK"] = "0"
-    try:
+    with _lib.tuning(splitk=0):
         y_plain = run_engine(blob, x)
-    finally:
-        os.environ.pop("MDE_SPLITK", None)
     m = depth_metrics(y_split, y_plain)
     print(f"split-K vs unsplit {encoder} {size}", m)
     # the fp32 reassociation is amplified by the downstream f16 roundings
@@ -194,88 +191,122 @@ def test_fc2_splitk_matches_unsplit(gpu, encoder, size):
     assert m["max_abs"] < 0.08 and m["rel_mean"] < 1.5e-3, m
 
 
-@pytest.mark.parametrize("encoder,size,B", [("vits", 98, 2), ("vitl", 518, 1)])
-def test_dpt_fork_bit_exact(gpu, encoder, size, B):
-    """Small grids run the reassemble + layerN_rn branch of taps 0..2 on a
-    side stream beside the encoder's later blocks (engine.hip dpt_fork, a
-    parallel branch of the captured graph).  Only the launch order changes:
-    the depth map must equal the one-stream forward bit for bit, in graph
-    replay and eager mode."""
-    cfg = weights.model_config(encoder, "metric")
-    sd = weights.synthetic_state_dict(cfg, 8)
-    blob = pack.pack_bytes(sd, cfg, size, size)
-    x = weights.synthetic_images(B, size, size, first_seed=31)
-    os.environ["MDE_DPT_FORK"] = "1"
-    try:
-        y_fork = run_engine(blob, x, graph=True)
-        y_fork_eager = run_engine(blob, x, graph=False)
-        os.environ["MDE_DPT_FORK"] = "0"
-        y_one = run_engine(blob, x, graph=True)
-    finally:
-        os.environ.pop("MDE_DPT_FORK", None)
-    assert np.isfinite(y_one).all()
-    assert np.array_equal(y_fork, y_one), "forked DPT branch (graph) must equal the one-stream forward"
-    assert np.array_equal(y_fork_eager, y_one), "forked DPT branch (eager) must equal the one-stream forward"
-
-
-@pytest.mark.parametrize("var,tile", [("MDE_GEMM_TILE", "big1"), ("MDE_GEMM_TILE", "128x128w8"),
-                                      ("MDE_GEMM_W16", "1")])
-def test_gemm_tile_variants_bit_exact(gpu, var, tile):
-    """ViT-L 518^2 B=1 (config 3's unit) with the small-grid GEMM tilings
-    (MDE_GEMM_TILE: tall 160/192-row tiles on a 3-deep ring, or 8 waves on
-    the 128^2 tile, or 64 x 128 small-grid tiles; MDE_GEMM_W16: 16 waves of
-    32 x 32 on the small-grid 128^2 tiles).  A tile's K loop runs in the same order whatever its
-    shape and the split-K slicing is unchanged, so the depth map must equal
-    the default tiling's bit for bit."""
+@pytest.mark.parametrize("switch", ["deep64", "w8small"])
+def test_gemm_small_grid_variants_bit_exact(gpu, switch):
+    """ViT-L 518^2 B=1 (config 3's unit) with a small-grid GEMM tiling switched
+    off (tuning.h: "deep64" = the 4-deep ring of the 64^2 tiles and split-K
+    slices, "w8small" = 8 waves on the 128^2 tiles of qkv / fc1 / the fc2
+    slices).  A tile's K loop runs in the same order whatever its ring depth or
+    wave count and the split-K slicing does not depend on either switch, so
+    the depth map must equal the default tiling's bit for bit."""
     cfg = weights.model_config("vitl", "metric")
     sd = weights.synthetic_state_dict(cfg, 12)
     blob = pack.pack_bytes(sd, cfg, 518, 518)
     x = weights.synthetic_images(1, 518, 518, first_seed=51)
     y_def = run_engine(blob, x)
-    os.environ[var] = tile
-    try:
+    with _lib.tuning(**{switch: 0}):
         y_var = run_engine(blob, x)
-    finally:
-        os.environ.pop(var, None)
     assert np.isfinite(y_def).all()
-    assert np.array_equal(y_var, y_def), f"{var}={tile} changed the result"
+    assert np.array_equal(y_var, y_def), f"{switch}=0 changed the result"
 
 
-@pytest.mark.parametrize("encoder,head", [("vitl", "metric"), ("vitl", "relative")])
-def test_gemm_stream_k(gpu, encoder, head):
-    """ViT-L 518^2 B=1 (config 3's unit): qkv (264 tiles of 128^2), fc1 (352)
-    and fc2 (88 tiles x 64 K-steps) under stream-K (gemm.hip gemm_sk_kernel):
-    256 workgroups take whole tiles for as many full rounds as the grid holds,
-    then equal shares of the remaining (tile, K-step) iterations; the last
-    contributor of a cut tile sums the fp32 partial slots in contributor
-    order.  Two runs (graph replay, then eager) must be bit-identical -- the
-    order is fixed and every launch leaves its arrival counters at zero --
-    and the map must match the whole-tile kernels (MDE_GEMM_SK=0) up to fp32
-    reassociation, the same bar as the split-K test above.  Opt-in
-    (MDE_GEMM_SK=1): measured slower than the whole-tile kernels."""
-    cfg = weights.model_config(encoder, head)
-    sd = weights.synthetic_state_dict(cfg, 14)
+def _oracle_chunks(sd, cfg, x, chunk=8):
+    from oracle import dav2_ref
+    torch.set_num_threads(min(32, os.cpu_count() or 1))
+    w = dav2_ref.to_torch(sd)
+    return np.concatenate([dav2_ref.forward(w, cfg, x[i:i + chunk]).numpy() for i in range(0, len(x), chunk)])
+
+
+@pytest.mark.parametrize("B", [32, 48])
+def test_engine_518_bench_batches_vs_oracle(gpu, B):
+    """The graphs the bench times (bench.py: ViT-S 518^2, B = 48 per GPU, a
+    context sized for exactly that batch, hipGraph replay): B = 48 runs the
+    8-wave 256-query attention (g256 = 6 x 48 x 6 >= 512) and the 256 x 128
+    8-wave residual tiles (t256 >= 512 from B = 32 on), which the B <= 8 tests
+    above never reach.  B = 32 is the first batch on the 256 x 128 residual
+    tiles.  Every map against the fp32 oracle at the DA-V2 bars
+    (verify_accuracy.py:54-55 thresholds are far looser)."""
+    cfg = weights.model_config("vits", "metric")
+    sd = weights.synthetic_state_dict(cfg, 1234)   # the bench's weights
+    x = weights.synthetic_images(B, 518, 518, first_seed=0)
+    y = run_engine(pack.pack_bytes(sd, cfg, 518, 518), x)
+    ref = _oracle_chunks(sd, cfg, x)
+    assert y.shape == (B, 518, 518)
+    check(y, ref, 20.0, f"518 B={B} (bench graph) vs oracle")
+    worst = max(depth_metrics(y[i:i + 1], ref[i:i + 1])["max_abs"] for i in range(B))
+    assert worst <= 0.003 * 20.0, worst
+
+
+def test_lnfold_matches_layernorm(gpu):
+    """Switch "lnfold" = 0 (read at context creation): norm1 / norm2 / the tap
+    norms as LayerNorm launches and the unfolded qkv / fc1 / project weights,
+    against the default folded engine -- both within the DA-V2 bars of the
+    oracle, and close to each other (one more f16 rounding of the normed
+    rows on the unfolded side)."""
+    from oracle import dav2_ref
+    cfg = weights.model_config("vits", "metric")
+    sd = weights.synthetic_state_dict(cfg, 808)
+    x = weights.synthetic_images(2, 518, 518, first_seed=70)
     blob = pack.pack_bytes(sd, cfg, 518, 518)
-    x = weights.synthetic_images(1, 518, 518, first_seed=61)
-    y_tiles = run_engine(blob, x)
-    os.environ["MDE_GEMM_SK"] = "1"  # opt-in (measured slower, DESIGN.md)
-    try:
-        y_sk = run_engine(blob, x, graph=True)
-        assert np.isfinite(y_sk).all()
-        assert np.array_equal(y_sk, run_engine(blob, x, graph=True)), "stream-K must be deterministic (graph replay)"
-        assert np.array_equal(y_sk, run_engine(blob, x, graph=False)), "stream-K must be deterministic (eager)"
-    finally:
-        os.environ.pop("MDE_GEMM_SK", None)
-    m = depth_metrics(y_sk, y_tiles)
-    print(f"stream-K vs whole tiles {encoder} {head}", m)
-    scale = float(np.abs(y_tiles).max())
-    if head == "metric":  # 0.08 m of the 20 m range, as above
-        assert m["max_abs"] < 0.004 * scale and m["rel_mean"] < 1.5e-3, m
-    else:
-        # the synthetic relative map is small (mean |y| ~ 1e-2), so the same
-        # absolute noise is a larger fraction of it: measured rel_mean 3.8e-3,
-        # max_abs 5.3e-3, corr 0.999993 (MI355X)
-        assert m["rel_mean"] < 1e-2 and m["corr"] > 0.9999, m
+    ref = dav2_ref.forward(dav2_ref.to_torch(sd), cfg, x).numpy()
+    y_fold = run_engine(blob, x)
+    with _lib.tuning(lnfold=0):
+        y_ln = run_engine(blob, x)
+    check(y_fold, ref, 20.0, "518 B=2 folded LN vs oracle")
+    check(y_ln, ref, 20.0, "518 B=2 LayerNorm launches vs oracle")
+    m = depth_metrics(y_fold, y_ln)
+    print("folded vs unfolded LN", m)
+    assert m["rel_mean"] < 1.5e-3 and m["corr"] >= CORR, m
+
+
+def test_enqueue_inside_caller_capture(gpu):
+    """A caller that captures its own stream (torch.cuda.graph) gets the
+    forward's kernels captured into its graph (engine.hip: no graph of ours
+    is launched inside a capture); replaying the caller's graph on new input
+    equals the engine's own result, and more distinct shapes than the
+    context's graph cache holds can go through it."""
+    cfg = weights.model_config("vits", "metric")
+    sd = weights.synthetic_state_dict(cfg, 5)
+    blob = pack.pack_bytes(sd, cfg, 98, 98)
+    xa = weights.synthetic_images(3, 98, 98, first_seed=90)
+    xb = weights.synthetic_images(3, 98, 98, first_seed=93)
+    ref_b = run_engine(blob, xb)
+    eng = Engine.from_bytes(blob, 0, profile=((1, 3, 98, 98), (3, 3, 98, 98), (3, 3, 98, 98)))
+    ctx = eng.create_execution_context()
+    xin = torch.from_numpy(xa).cuda()
+    out = torch.empty(3, 98, 98, device="cuda")
+    ctx.set_input_shape("input", xa.shape)
+    ctx.set_tensor_address("input", xin.data_ptr())
+    ctx.set_tensor_address("output", out.data_ptr())
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        ctx.execute_async_v3(s.cuda_stream)   # warm (eager outside capture: graph mode, own cache)
+    torch.cuda.synchronize()
+    with torch.cuda.graph(g, stream=s):
+        ctx.execute_async_v3(s.cuda_stream)
+    xin.copy_(torch.from_numpy(xb))
+    g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(out.cpu().numpy(), ref_b), "captured forward must equal the engine's own"
+    # more (batch, address) keys than the context caches (kMaxGraphs = 8), all
+    # captured into caller graphs
+    graphs = []
+    for i in range(10):
+        o = torch.empty(3, 98, 98, device="cuda")
+        ctx.set_tensor_address("output", o.data_ptr())
+        gi = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(gi, stream=s):
+            ctx.execute_async_v3(s.cuda_stream)
+        graphs.append((gi, o))
+    for gi, o in graphs:
+        gi.replay()
+    torch.cuda.synchronize()
+    for gi, o in graphs:
+        assert np.array_equal(o.cpu().numpy(), ref_b)
+    ctx.destroy()
+    eng.destroy()
 
 
 @pytest.mark.parametrize("encoder", ["vits", "vitl"])

@@ -183,7 +183,7 @@ def test_attention_key_groups(gpu, cfg, B, H, T, spiky):
 @pytest.mark.parametrize("cfg", ["8", "4", "8q2", "4q2", "8r3", "4r4", "4s2", "4s3"])
 @pytest.mark.parametrize("B,H,T", [(2, 3, 300), (1, 6, 1370)])
 def test_attention_tuning_configs(gpu, cfg, B, H, T):
-    """Every launch shape MDE_ATTN_CFG can force (mde_op_attention_cfg): 8 / 4
+    """Every launch shape mde_op_attention_cfg can force: 8 / 4
     waves, two query sub-tiles per wave (q2), 3- and 4-deep K/V rings, split-KV
     over workgroups with the combine kernel -- the same numbers as the policy's
     shapes, against torch."""
@@ -305,21 +305,18 @@ def test_conv_narrow_tiles_bit_exact(gpu, h, cin, cout):
     channels, 64 of > 64): against torch, and bit for bit against the wide
     tiles (MDE_CONV_NARROW=0) -- an output channel's K order is the tile's,
     whatever the tile width."""
-    import os
     x = rn(1, cin, h, h)
     wt, b = rn(cout, cin, 3, 3, scale=(9 * cin) ** -0.5), rn(cout, scale=0.02)
     ref = F.relu(F.conv2d(F.relu(x.half().float()), wt.half().float(), b, padding=1))
     wp = conv_w(wt).to(gpu)
     xg, bg = nhwc(x).half().to(gpu), b.to(gpu)
+    from monocular_depth_estimation_trt_amd import _lib
     got = []
-    for flag in ("1", "0"):
-        os.environ["MDE_CONV_NARROW"] = flag
-        try:
+    for flag in (1, 0):
+        with _lib.tuning(conv_narrow=flag):
             out = torch.empty(1, h, h, cout, dtype=torch.float16, device=gpu)
             op("mde_op_conv3x3", ptr(xg), 1, h, h, cin, ptr(wp), wp.shape[1], cout, 1, 1, ptr(bg), 1, None, None,
                ptr(out), stream())
-        finally:
-            os.environ.pop("MDE_CONV_NARROW", None)
         got.append(out)
     close(nchw(got[0]), ref, 1e-2, 1e-2, f"conv narrow tiles {h}^2 {cin}->{cout}")
     assert torch.equal(got[0], got[1]), "narrow conv tiles must equal the wide ones bit for bit"
@@ -454,38 +451,64 @@ def test_depth_head(gpu, metric):
                                                    (1, 9, 40, 16, 70, 32, 0), (1, 1, 1, 1, 1, 32, 1),
                                                    # grids past the persistent size at 64 / 128 channels
                                                    (2, 148, 148, 296, 296, 64, 0), (2, 100, 100, 200, 200, 128, 1)])
-def test_upconv_matches_conv3(gpu, monkeypatch, B, sh, sw, uh, uw, cin, head):
-    """The separable upsampling conv (conv.hip upconv_kernel, persistent when
-    the grid exceeds what the chip holds at once) against the 4-tap
-    conv3_kernel it replaces (MDE_UPCONV=0): the same two-level f16
-    blend in the same order, so at 32 input channels (one chunk, same MFMA
-    order) the outputs are bit-identical; wider inputs sum 32-channel chunks
-    in another order (fp32), within one f16 ulp."""
+def test_upconv_matches_conv3(gpu, B, sh, sw, uh, uw, cin, head):
+    """The separable upsampling conv (conv.hip upconv_kernel: one tile per
+    workgroup on small grids, persistent when the grid exceeds what the chip
+    holds at once -- the last two cases) against the 4-tap conv3_kernel it
+    replaces (switch "upconv" = 0): the same two-level f16 blend in the same
+    order, so at 32 input channels (one chunk, same MFMA order) the outputs
+    are bit-identical; wider inputs sum 32-channel chunks in another order
+    (fp32), within one f16 ulp."""
+    from monocular_depth_estimation_trt_amd import _lib
     x = rn(B, cin, sh, sw)
     w1, b1 = rn(32, cin, 3, 3, scale=(9 * cin) ** -0.5), rn(32, scale=0.02)
     w2 = rn(32, scale=32 ** -0.5)
     wp = conv_w(w1).to(gpu)
     xin = nhwc(x).half().to(gpu)
     outs = []
-    for flag, persist in (("0", "1"), ("1", "1"), ("1", "0")):  # conv3_kernel, persistent upconv, one tile per workgroup
-        monkeypatch.setenv("MDE_UPCONV", flag)
-        monkeypatch.setenv("MDE_UPCONV_PERSIST", persist)
-        if head:
-            out = torch.empty(B, uh, uw, device=gpu)
-            op("mde_op_depth_head", ptr(xin), B, sh, sw, cin, uh, uw, ptr(wp), wp.shape[1], ptr(b1.to(gpu)),
-               ptr(w2.to(gpu)), 0.05, 1, 20.0, ptr(out), stream())
-        else:
-            out = torch.empty(B, uh, uw, 32, dtype=torch.float16, device=gpu)
-            op("mde_op_conv3x3_up", ptr(xin), B, sh, sw, cin, uh, uw, ptr(wp), wp.shape[1], 32, ptr(b1.to(gpu)), 0,
-               ptr(out), stream())
-        torch.cuda.synchronize()
+    for flag in (0, 1):  # conv3_kernel, upconv_kernel
+        with _lib.tuning(upconv=flag):
+            if head:
+                out = torch.empty(B, uh, uw, device=gpu)
+                op("mde_op_depth_head", ptr(xin), B, sh, sw, cin, uh, uw, ptr(wp), wp.shape[1], ptr(b1.to(gpu)),
+                   ptr(w2.to(gpu)), 0.05, 1, 20.0, ptr(out), stream())
+            else:
+                out = torch.empty(B, uh, uw, 32, dtype=torch.float16, device=gpu)
+                op("mde_op_conv3x3_up", ptr(xin), B, sh, sw, cin, uh, uw, ptr(wp), wp.shape[1], 32, ptr(b1.to(gpu)),
+                   0, ptr(out), stream())
+            torch.cuda.synchronize()
         outs.append(out.float().cpu())
-    old, new, single = outs
-    assert torch.equal(new, single), (new - single).abs().max()
+    old, new = outs
     if cin == 32:
         assert torch.equal(old, new), (old - new).abs().max()
     else:
         assert torch.allclose(old, new, rtol=2e-3, atol=2e-3), (old - new).abs().max()
+
+
+@pytest.mark.parametrize("M,N,K,act", [(1370, 3072, 1024, 2), (2740, 1024, 4096, 0), (600, 768, 768, 0)])
+def test_gemm256_modes_match(gpu, M, N, K, act):
+    """Switch "gemm256" (tuning.h): 0 never the 256^2 phase-pipelined kernel,
+    1 the auto policy, 2 whenever legal.  Every mode against torch, and the
+    modes against each other (a different tile sums K in the same 64-deep
+    order per output, so 0 and 2 agree to fp32 rounding of the epilogue)."""
+    from monocular_depth_estimation_trt_amd import _lib
+    a = rn(M, K)
+    w, b = rn(N, K, scale=K ** -0.5), rn(N, scale=0.02)
+    ref = a.half().float() @ w.half().float().t() + b
+    if act == 2:
+        ref = F.gelu(ref)
+    wp = torch.zeros(-(-N // 128) * 128, -(-K // 64) * 64, dtype=torch.float16)
+    wp[:N, :K] = w.half()
+    wp, ag, bg = wp.to(gpu), a.half().to(gpu), b.to(gpu)
+    outs = []
+    for mode in (0, 1, 2):
+        with _lib.tuning(gemm256=mode):
+            out = torch.empty(M, N, dtype=torch.float16, device=gpu)
+            op("mde_op_linear", ptr(ag), K, ptr(wp), wp.shape[1], M, N, K, ptr(bg), act, ptr(out), N, stream())
+            torch.cuda.synchronize()
+        close(out, ref, 1e-2, 1e-2, f"linear gemm256={mode} {M}x{N}x{K}")
+        outs.append(out.float().cpu())
+    assert torch.allclose(outs[0], outs[2], rtol=2e-3, atol=2e-3), (outs[0] - outs[2]).abs().max()
 
 
 def test_bad_arguments_raise(gpu):

@@ -1,9 +1,10 @@
 """VGGT's depth path on the HIP engine, through the C
 ABI, against the oracle (oracle/vggt_ref.py; partially pinned, see its
 header): the "tiny" preset (98x98, 7x7 patches, D 128) for one and two
-frames, and "vggt_1b_shallow" -- every kernel shape of VGGT-1B at 518^2
+frames, "vggt_1b_shallow" -- every kernel shape of VGGT-1B at 518^2
 (D 1024, 16 heads, T 1374, the 2048-wide taps, the full DPT decoder) with
-2 + 4 blocks so the CPU oracle finishes in seconds.
+2 + 4 blocks -- and the bench model "vggt_1b" itself (24 + 24 blocks, one and
+two frames; the oracle takes ~10 s per frame on the box's cores).
 
 Tolerance (fp16 operands, fp32 accumulation vs the fp32 oracle), stated
 per case in _check's callers at ~3x the measured error: depth rel_mean <=
@@ -73,13 +74,13 @@ def tiny_s2(gpu):
 # widths at 518^2 9.3e-4 / 0.0055, corr >= 0.999997 everywhere), so a
 # numerical regression of a few x fails.  Against the oracle only: the VGGT
 # aggregator is parity-unpinned.
-def _check(y, ref, what, rel=2e-3, max_abs=0.02):
+def _check(y, ref, what, rel=2e-3, max_abs=0.02, corr=0.99999):
     m = depth_metrics(y, ref)
-    print(what, m, "ref range", float(ref.min()), float(ref.max()))
+    print(what, m, "ref range", float(ref.min()), float(ref.max()), flush=True)
     assert y.shape == ref.shape, (y.shape, ref.shape)
     assert np.isfinite(y).all()
     assert m["rel_mean"] <= rel, m
-    assert m["corr"] >= 0.99999, m
+    assert m["corr"] >= corr, m
     assert m["max_abs"] <= max_abs, m
 
 
@@ -107,6 +108,22 @@ def test_vggt_1b_shallow_518_matches_oracle(gpu):
     cfg, sd, x, ref, blob = _case("vggt_1b_shallow", 1, 1)
     assert ref.shape == (1, 1, 518, 518, 1)
     _check(run_engine(blob, x), ref, "vggt_1b_shallow 518 B=1", rel=3e-3, max_abs=0.017)
+
+
+@pytest.mark.parametrize("frames", [1, 2])
+def test_vggt_1b_full_518_matches_oracle(gpu, frames):
+    """The bench model itself (bench.py --model vggt: "vggt_1b" = 24 DINOv2
+    blocks + 24 frame/global block pairs, the DPT taps after aggregator
+    blocks 4, 11, 17, 23 -- weights_vggt.py), B = 1 at 518^2, one frame and
+    two (global attention over 2 x 1374 tokens, special-token set 1 on frame
+    1), against the oracle: the tap indexing and the error growth over the
+    real depth, which the shallow preset cannot show.  Aggregator parity
+    unpinned (oracle/vggt_ref.py header: the reference holds nothing to pin
+    it against); the bars are ~3x the error measured on MI355X."""
+    cfg, sd, x, ref, blob = _case("vggt_1b", 1, frames)
+    assert ref.shape == (1, frames, 518, 518, 1)
+    _check(run_engine(blob, x), ref, f"vggt_1b (24 + 24 blocks) 518 B=1 S={frames}", rel=6e-3, max_abs=0.05,
+           corr=0.9999)
 
 
 def test_engine_rejects_bad_shapes(tiny_b2):
