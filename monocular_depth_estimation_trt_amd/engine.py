@@ -99,8 +99,14 @@ class Engine:
     @classmethod
     def from_bytes(cls, blob: bytes, device: int = 0, **kw) -> "Engine":
         h = C.c_void_p()
-        buf = C.create_string_buffer(blob, len(blob))
-        call("mde_engine_load_memory", C.cast(buf, C.c_void_p), len(blob), int(device), C.byref(h))
+        # the bytes object itself is the argument (ctypes passes its buffer):
+        # a create_string_buffer copy passed through C.cast forms a reference
+        # cycle, and the whole packed blob (53 MB ViT-S, 671 MB ViT-L) then
+        # waited for a cyclic-GC pass to be freed -- which landed inside the
+        # batch-1 timed loop as a 7.7 ms (ViT-S) / ~76 ms (ViT-L) sample
+        # (bench.py b1_gc_in_loop, gpurun_out/r4s1)
+        blob = bytes(blob) if not isinstance(blob, bytes) else blob
+        call("mde_engine_load_memory", blob, len(blob), int(device), C.byref(h))
         return cls(h.value, device, **kw)
 
     @property
