@@ -130,63 +130,55 @@ struct SplitWs {
 // O^T (32 fp32) + (m, l)
 constexpr int MERGE_WAVE_B = 64 * 34 * 4;
 
-// LDS bytes of one attention workgroup shape (ring, or the key-group merge area)
-template <int NW, int R, int NS, bool MB>
-constexpr int attn_lds_bytes() {
-  constexpr int NWQ = NW / NS;
-  constexpr int RING_B = R * NS * SLOT, MERGE_B = (MB ? 0 : (NS - 1)) * NWQ * MERGE_WAVE_B;
-  return RING_B > MERGE_B ? RING_B : MERGE_B;
-}
-
-// One workgroup's work: NW waves over the queries [q0, q0 + BQ) of sequence-
-// head bh0 (NS = 1), or NS groups of NW / NS query waves --
-//  * key groups (NS > 1, !MB): every group on the same queries of bh0, group g
-//    walking the g-th slice of the key tiles with its own K / V^T ring slots;
-//    the groups' (O, m, l) merge through LDS after the loop (the split-KV
-//    parallelism without the fp32 workspace round trip or a second kernel);
-//  * head groups (MB): group g on the queries [q0, ..) of sequence-head
-//    bh0 + g with all the keys, each with its own ring slots and its own
-//    output -- the packed query tails (attn_packed_kernel).
-// QS = 2: each wave owns two 32-query sub-tiles; every K / V^T fragment read
-// feeds both, and one sub-tile's softmax overlaps the other's MFMAs.
-// SPLIT: this workgroup's key range is split blockIdx.z of ws.tiles tiles.
-template <int NW, bool SPLIT, int R, int QS, int NS, bool MB>
-MDE_DEV void attn_block(char* __restrict__ smem, const f16* __restrict__ q, const f16* __restrict__ k,
-                        const f16* __restrict__ vt, f16* __restrict__ o, int H, int T, int Tpad, int ldo, SplitWs ws,
-                        int bh0, int q0, int BH) {
+template <int NW, bool SPLIT, int R, int QS = 1, int NS = 1>
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(QS == 2 ? 2 : 4, 8)))
+attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16* __restrict__ vt,
+                f16* __restrict__ o, int H, int T, int Tpad, int ldo, SplitWs ws) {
+  // QS = 2: each wave owns two 32-query sub-tiles; every K / V^T fragment
+  // read feeds both, and one sub-tile's softmax overlaps the other's MFMAs.
+  // NS > 1 (small grids): the workgroup's waves form NS key GROUPS of NW / NS
+  // query waves; group g walks the g-th slice of the key tiles for the same
+  // queries, each with its own K / V^T ring slots, and the groups' (O, m, l)
+  // merge through LDS after the loop -- the split-KV parallelism without the
+  // fp32 workspace round trip or a second kernel.
   static_assert(QS == 1 || (QS == 2 && !SPLIT && NS == 1), "query sub-tiles per wave");
-  static_assert(NS == 1 || (!SPLIT && R == 2), "key / head groups");
-  static_assert(!MB || NS > 1, "head groups");
-  constexpr int NWQ = NW / NS;       // query waves per group
+  static_assert(NS == 1 || (!SPLIT && R == 2), "key groups");
+  constexpr int NWQ = NW / NS;       // query waves per key group
+  constexpr int BQ = QW * NWQ * QS;  // queries per workgroup
   constexpr int INS = 8 / NWQ;       // glds instructions per wave per image (8 per 64-row image)
   constexpr int PER_TILE = 2 * INS;  // vmcnt entries one tile adds per wave (K + V^T)
   static_assert(NWQ * NS == NW && (NWQ == 1 || NWQ == 2 || NWQ == 4 || NWQ == 8 || (NWQ == 3 && R == 2)),
-                "waves per group");
+                "waves per key group");
   static_assert(NW == 4 || NW == 8 || (NS > 1 && (NW == 6 || NW == 12 || NW == 16)), "waves per workgroup");
   static_assert(R >= 2 && R <= 4, "ring depth");
   constexpr int DIST = R - 1;  // tiles in flight ahead of the one computed
+  constexpr int RING_B = R * NS * SLOT, MERGE_B = (NS - 1) * NWQ * MERGE_WAVE_B;
+  __shared__ __attribute__((aligned(16))) char smem[RING_B > MERGE_B ? RING_B : MERGE_B];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int grp = NS > 1 ? wave_all / NWQ : 0;   // key / head group
+  const int grp = NS > 1 ? wave_all / NWQ : 0;   // key group
   const int wave = wave_all - grp * NWQ;         // query wave within the group
-  // a head group past the last sequence-head loads bh0's tiles (valid
-  // addresses, uniform vmcnt) and computes nothing
-  const bool bh_ok = !MB || bh0 + grp < BH;
-  const int bh = MB && bh_ok ? bh0 + grp : bh0;
+  // XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs
+  // (linear id % 8 shares an L2); remap so each XCD takes a contiguous run
+  // of (head, query block) pairs and a head's K/V^T is fetched into one L2,
+  // not eight (PMC: 4.5x the algorithmic bytes without it).  Bijective.
+  const int nqb = gridDim.x, nwg = gridDim.x * gridDim.y;
+  int lin = blockIdx.y * nqb + blockIdx.x;
+  lin = xcd_remap(lin, nwg);
+  const int bh = lin / nqb;
   const int b = bh / H, h = bh - (bh / H) * H;
-  const int qbase = q0 + wave * QW * QS;
-  const bool active = bh_ok && qbase < T;  // wave-uniform: a wave past the last query only helps load
+  const int qbase = (lin - bh * nqb) * BQ + wave * QW * QS;
+  const bool active = qbase < T;  // wave-uniform: a wave past the last query only helps load
   const int l31 = lane & 31, hh = lane >> 5;
 
   // key tiles [kt0, kt1) of this workgroup / key group (all of them unless
   // split); every group steps ktl - kt0 times (uniform barrier count)
   const int nkt_all = (T + KT - 1) / KT;
-  constexpr int NKG = MB ? 1 : NS;            // key groups
-  const int gper = (nkt_all + NKG - 1) / NKG;  // tiles per key group
-  const int kt0 = SPLIT ? (int)blockIdx.z * ws.tiles : (MB ? 0 : grp * gper);
+  const int gper = (nkt_all + NS - 1) / NS;  // tiles per key group
+  const int kt0 = SPLIT ? (int)blockIdx.z * ws.tiles : grp * gper;
   const int kt1 = SPLIT ? min(nkt_all, kt0 + ws.tiles) : min(nkt_all, kt0 + gper);
-  const int ktl = NKG > 1 ? kt0 + gper : kt1;
+  const int ktl = NS > 1 ? kt0 + gper : kt1;
 
   const f16* qb = q + (size_t)bh * Tpad * 64;
   const f16* kb = k + (size_t)bh * Tpad * 64;
@@ -383,7 +375,7 @@ MDE_DEV void attn_block(char* __restrict__ smem, const f16* __restrict__ q, cons
   if (R > 2 && kt + 1 < ktl) step(kt + 1, S2{}, NF{});
   if (R > 3 && kt + 2 < ktl) step(kt + 2, S3{}, NF{});
 
-  if constexpr (NS > 1 && !MB) {
+  if constexpr (NS > 1) {
     // merge the key groups: groups 1.. park (O^T, m, l) in LDS (the ring is
     // free: every wave's last LDS read came before the last step's barrier,
     // and that step waited out every load), group 0 rescales to the common
@@ -436,7 +428,7 @@ MDE_DEV void attn_block(char* __restrict__ smem, const f16* __restrict__ q, cons
   if constexpr (SPLIT) {
     // unnormalised O^T (relative to m_run) and (m, l) of this key range
     const float lt = swap_sum(l_run[0]);
-    const size_t row = ((size_t)blockIdx.z * BH + bh) * ws.Tq + qi;
+    const size_t row = ((size_t)blockIdx.z * gridDim.y + bh) * ws.Tq + qi;
     float* orow = ws.o + row * 64;
 #pragma unroll
     for (int db = 0; db < 2; ++db)
@@ -480,53 +472,6 @@ MDE_DEV void attn_block(char* __restrict__ smem, const f16* __restrict__ q, cons
   }
 }
 
-// Grid (query blocks, B*H[, splits]): one attn_block per workgroup.
-template <int NW, bool SPLIT, int R, int QS = 1, int NS = 1>
-__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(QS == 2 ? 2 : 4, 8)))
-attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16* __restrict__ vt,
-                f16* __restrict__ o, int H, int T, int Tpad, int ldo, SplitWs ws) {
-  __shared__ __attribute__((aligned(16))) char smem[attn_lds_bytes<NW, R, NS, false>()];
-  constexpr int BQ = QW * (NW / NS) * QS;  // queries per workgroup
-  // XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs
-  // (linear id % 8 shares an L2); remap so each XCD takes a contiguous run
-  // of (head, query block) pairs and a head's K/V^T is fetched into one L2,
-  // not eight (PMC: 4.5x the algorithmic bytes without it).  Bijective.
-  const int nqb = gridDim.x, nwg = gridDim.x * gridDim.y;
-  const int lin = xcd_remap(blockIdx.y * nqb + blockIdx.x, nwg);
-  const int bh = lin / nqb;
-  attn_block<NW, SPLIT, R, QS, NS, false>(smem, q, k, vt, o, H, T, Tpad, ldo, ws, bh, (lin - bh * nqb) * BQ,
-                                          gridDim.y);
-}
-
-// Packed query tails (large grids, T not a multiple of the NW x 32-query
-// block): the nfull whole blocks of every sequence-head run as above; the
-// tails (T - nfull * BQ queries, at most NW / 2 waves' worth) of TG
-// consecutive sequence-heads share ONE workgroup as TG head groups of NW / TG
-// waves (attn_block MB).  ViT-S 518^2: 1370 = 5 x 256 + 90 -- the sixth block
-// of each (image, head) held 3 live waves of 8 for a whole key loop; two
-// tails per workgroup halve those workgroups (B = 48: 1728 -> 1584).  Work
-// order: per group of TG sequence-heads, their TG x nfull whole blocks then
-// their shared tail block, so every XCD's contiguous run (xcd_remap) mixes
-// tails in evenly and keeps a head's K / V^T in one L2.
-template <int NW, int R, int TG>
-__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4, 8)))
-attn_packed_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16* __restrict__ vt,
-                   f16* __restrict__ o, int H, int T, int Tpad, int ldo, int BH, int nfull) {
-  constexpr int L0 = attn_lds_bytes<NW, R, 1, false>(), L1 = attn_lds_bytes<NW, 2, TG, true>();
-  __shared__ __attribute__((aligned(16))) char smem[L0 > L1 ? L0 : L1];
-  constexpr int BQ = QW * NW;
-  const int per = TG * nfull + 1;  // work items per group of TG sequence-heads
-  const int lin = xcd_remap(blockIdx.x, gridDim.x);
-  const int g = lin / per, r = lin - g * per;
-  if (r < TG * nfull) {
-    const int bh = g * TG + r / nfull;
-    if (bh >= BH) return;  // workgroup-uniform, before any load or barrier
-    attn_block<NW, false, R, 1, 1, false>(smem, q, k, vt, o, H, T, Tpad, ldo, SplitWs{}, bh, (r % nfull) * BQ, BH);
-  } else {
-    attn_block<NW, false, 2, 1, TG, true>(smem, q, k, vt, o, H, T, Tpad, ldo, SplitWs{}, g * TG, nfull * BQ, BH);
-  }
-}
-
 // Merge S split-KV partials: one thread per (sequence*head, query, 8 dims).
 // O = sum_s 2^(m_s - m) O_s / sum_s 2^(m_s - m) l_s, m = max_s m_s.
 __global__ void __launch_bounds__(256) attn_combine_kernel(SplitWs ws, int S, int BH, int H, int T, int ldo,
@@ -562,23 +507,6 @@ __global__ void __launch_bounds__(256) attn_combine_kernel(SplitWs ws, int S, in
   for (int j = 0; j < 8; ++j) v[j] = (f16)(acc[j] * inv);
   const int b = bh / H, h = bh - b * H;
   *reinterpret_cast<f16x8*>(o + ((size_t)b * T + qi) * ldo + h * 64 + 8 * d8) = v;
-}
-
-// the packed-tail launch when the last query block holds at most NW / 2
-// waves' worth of live queries (attn_packed_kernel); false: not applicable
-template <int NW, int R>
-bool run_attn_packed(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T, int Tpad, int ldo,
-                     hipStream_t st) {
-  constexpr int BQ = QW * NW, TG = 2;
-  const int nfull = T / BQ, tail = T - nfull * BQ;
-  if (nfull < 1 || tail == 0 || (tail + QW - 1) / QW > NW / TG) return false;
-  const int BH = B * H, groups = (BH + TG - 1) / TG;
-  const long long nwg = (long long)groups * (TG * nfull + 1);
-  if (nwg >= (1ll << 31)) return false;
-  hipLaunchKernelGGL((attn_packed_kernel<NW, R, TG>), dim3((unsigned)nwg), dim3(NW * 64), 0, st,
-                     reinterpret_cast<const f16*>(q), reinterpret_cast<const f16*>(k), reinterpret_cast<const f16*>(vt),
-                     reinterpret_cast<f16*>(o), H, T, Tpad, ldo, BH, nfull);
-  return true;
 }
 
 template <int NW, int R, int QS = 1>
@@ -644,7 +572,6 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
   // a forced launch shape (mde_op_attention_cfg: tests, tuning)
   const char* forced = cfg && cfg[0] ? cfg : nullptr;
   int nw = 0, split = 1, ring = ATTN_RING, qs2 = 0, groups = 1;
-  bool packed = false, nopack = false;
   if (forced) {
     nw = atoi(forced);
     const char* sp = strchr(forced, 's');
@@ -654,8 +581,6 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
     qs2 = strstr(forced, "q2") != nullptr;
     const char* gp = strchr(forced, 'g');  // "<waves>g<groups>": in-workgroup key groups
     if (gp) groups = atoi(gp + 1);
-    packed = strchr(forced, 'p') != nullptr;   // "8p": packed query tails
-    nopack = strchr(forced, 'u') != nullptr;   // "8u": unpacked (every block on its own)
   }
   if (nw != 4 && nw != 8 && !(groups > 1 && (nw == 6 || nw == 12 || nw == 16))) {
     // 256-query workgroups share each K/V^T tile over 8 waves once the grid
@@ -700,10 +625,6 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
   if (nw == 8) {
     if (ring == 4) return run_attn<8, 4>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, split, st);
     if (ring == 3) return run_attn<8, 3>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, split, st);
-    // the policy's large grids (and cfg "8p"): the last, partial query block of
-    // two sequence-heads packed into one workgroup
-    if (split <= 1 && (!forced || packed) && !nopack && run_attn_packed<8, 2>(q, k, vt, o, B, H, T, Tpad, ldo, st))
-      return hipGetLastError();
     return run_attn<8, 2>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, split, st);
   }
   if (ring == 4) return run_attn<4, 4>(q, k, vt, o, B, H, T, Tpad, ldo, ws, ws_bytes, split, st);
