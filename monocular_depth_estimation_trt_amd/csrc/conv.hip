@@ -84,8 +84,12 @@ constexpr int TH = 8, TW = 16;
 // are staged once with the patch, so the tap loop runs without a barrier --
 // the head convs (32 output channels) otherwise pay 10 barriers for 36 MFMAs
 // per wave.
+// 4-wave tiles of the plain (non-upsampling) conv held to 128 registers: the
+// 64-channel RCU conv (CK 64) otherwise allocates 82 VGPRs + 48 AGPRs = three
+// waves per SIMD; at four its 39 KB of LDS still lets four workgroups share a CU
 template <int BN, int WM, int WN, int CK, int S, bool UP, int EM, bool BRES = false>
-__global__ void __launch_bounds__(WM * WN * 64) conv3_kernel(const GemmParams p) {
+__global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(WM * WN == 4 && !UP ? 4 : 1)))
+conv3_kernel(const GemmParams p) {
   constexpr int NW = WM * WN, NT = NW * 64;
   constexpr int BM = TH * TW;
   constexpr int TM = BM / (WM * 16), TN = BN / (WN * 16);

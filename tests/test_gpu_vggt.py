@@ -119,11 +119,13 @@ def test_vggt_1b_full_518_matches_oracle(gpu, frames):
     1), against the oracle: the tap indexing and the error growth over the
     real depth, which the shallow preset cannot show.  Aggregator parity
     unpinned (oracle/vggt_ref.py header: the reference holds nothing to pin
-    it against); the bars are ~3x the error measured on MI355X."""
+    it against); the bars are ~3x the error measured on MI355X
+    (gpurun_out r4s3: S=1 rel 7.7e-4, max_abs 0.0086, corr 0.9999947; S=2
+    7.7e-4 / 0.0088 / 0.9999947; depth range 0.39-4.35)."""
     cfg, sd, x, ref, blob = _case("vggt_1b", 1, frames)
     assert ref.shape == (1, frames, 518, 518, 1)
-    _check(run_engine(blob, x), ref, f"vggt_1b (24 + 24 blocks) 518 B=1 S={frames}", rel=6e-3, max_abs=0.05,
-           corr=0.9999)
+    _check(run_engine(blob, x), ref, f"vggt_1b (24 + 24 blocks) 518 B=1 S={frames}", rel=2.5e-3, max_abs=0.026,
+           corr=0.99998)
 
 
 def test_engine_rejects_bad_shapes(tiny_b2):

@@ -54,6 +54,19 @@ VARIANTS = {
         ("""  const int wave = wave_all - grp * NWQ;         // query wave within the group""",
          """  const int wave = wave_all - grp * NWQ;         // query wave within the group
   if (NW == 8 && NS == 1 && wave_all >= 4) __builtin_amdgcn_s_setprio(1);""", 1)]),
+    # candidate (not an ablation): batch-1 stores / qkv whose 128^2 grid
+    # overhangs the CUs by a partial round (ViT-L B=1 qkv 264, fc1 352 tiles)
+    # on 256 x 128 tiles (8 waves of 64 x 64, BK 32 x 3 stages, two per CU):
+    # one round, 25 % fewer L2 -> LDS bytes per FLOP.  Measured slower (r4s3,
+    # same box: ViT-L B=1 3.19 -> 3.32 ms; qkv 0.612 -> 0.702, fc1 0.626 ->
+    # 0.696 ms per forward)
+    "gemm_wide_small": ("gemm.hip", [
+        ("""        if (w8small(big)) return run<128, 128, 2, 4, AM, EM>(p, st);""",
+         """        if (w8small(big)) {
+          const long long t2 = (long long)((p.M + 255) / 256) * ((p.N + 127) / 128);
+          if (t2 <= 256 && p.M >= 256) return run<256, 128, 4, 2, AM, EM, 32>(p, st);
+          return run<128, 128, 2, 4, AM, EM>(p, st);
+        }""", 1)]),
     # GEMM main loop only: the epilogue returns unless a NaN appears (r02's
     # MDE_EXP_NOEPI, profiles/r02_v10_epilogue_cost_*)
     "gemm_noepi": ("gemm.hip", [
