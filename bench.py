@@ -76,6 +76,7 @@ def measured_peak(kernel_class: str):
     return d.get(f"mfma_f16_{shape}_tflops"), shape
 ENC_LABEL = {"vits": "ViT-S", "vitb": "ViT-B", "vitl": "ViT-L"}
 REF_B1_FPS = 232.11         # RTX 3080 TRT fp16, BASELINE.md
+REF_B1_FP32_FPS = 88.29     # RTX 3080 TRT fp32 (the reference's default build), reports/tune/fp32_depth_anything_v2.json
 REF_B1_U8_FPS = 294.07      # same, uint8-NHWC input engine (reports/uint8_ab/depth_anything_v2.json)
 REF_DP_B1_FPS = 4.13        # Depth Pro 1536^2 TRT fp16, RTX 3080 (242.12 ms, BASELINE.md / SURVEY.md 6)
 REF_VGGT_B1_FPS = 19.02     # VGGT 518^2 S=1 TRT fp16, RTX 3080 (52.58 ms, BASELINE.md / SURVEY.md 6)
@@ -97,6 +98,8 @@ def parse(argv=None):
                    help="shard this many items over the ranks instead (strong scaling; config 3: 8)")
     p.add_argument("--frames", type=int, default=1, help="vggt: frames per batch item (the packed S)")
     p.add_argument("--encoder", default="vits", choices=["vits", "vitb", "vitl"])
+    p.add_argument("--precision", default="fp16", choices=["fp16", "fp32"],
+                   help="DA-V2 engine precision (get_engine's; fp32 = the exact-fp32 encoder)")
     p.add_argument("--size", type=int, default=518)
     p.add_argument("--b1-iters", type=int, default=100)
     p.add_argument("--b1-warmup", type=int, default=20)
@@ -298,6 +301,7 @@ class Workload:
         synthetic item seeds from `first` on."""
         import torch
         self.frames = 1
+        self.precision = "fp16"
         self.input_name = "input"
         if a.model == "depth_pro":
             from monocular_depth_estimation_trt_amd import pack_depth_pro as PD
@@ -344,11 +348,12 @@ class Workload:
             self.B = B
             self.cfg = weights.model_config(a.encoder, "metric")
             self.sd = weights.synthetic_state_dict(self.cfg, 1234)
-            self.blob = pack.pack_bytes(self.sd, self.cfg, S, S)
+            self.precision = a.precision
+            self.blob = pack.pack_bytes(self.sd, self.cfg, S, S, precision=a.precision)
             self.images = lambda n, seed: weights.synthetic_images(n, S, S, first_seed=seed)  # noqa: E731
             self.outs = {"output": (B, S, S)}
             self.gflop = total_flops(self.cfg, S, S) / 1e9
-            self.ref_fps = REF_B1_FPS
+            self.ref_fps = REF_B1_FPS if a.precision == "fp16" else REF_B1_FP32_FPS
             self.label = f"DA-V2 {ENC_LABEL.get(a.encoder, a.encoder)}"
             self.workload = (f"Depth Anything V2 {a.encoder} {S}x{S} metric head, forward, {a.per_gpu_desc}, "
                              f"inputs resident in HBM, hipGraph replay")
@@ -360,9 +365,11 @@ class Workload:
 
     def b1_legs(self, a, dev):
         res = b1_reference_method(self.blob, dev, self.images(1, 0), a.b1_warmup, a.b1_iters, self.ref_fps)
-        if a.model == "depth_anything_v2":
+        if a.model == "depth_anything_v2" and self.precision == "fp16":
+            # (the reference's uint8 A/B is an fp16 engine: reports/uint8_ab/depth_anything_v2.json)
             from monocular_depth_estimation_trt_amd import pack, weights
-            blob_u8 = pack.pack_bytes(self.sd, self.cfg, self.S, self.S, input_format="uint8_nhwc")
+            blob_u8 = pack.pack_bytes(self.sd, self.cfg, self.S, self.S, input_format="uint8_nhwc",
+                                      precision=self.precision)
             res.update(b1_reference_method(blob_u8, dev, weights.synthetic_images_u8(1, self.S, self.S, first_seed=0),
                                            a.b1_warmup, a.b1_iters, REF_B1_U8_FPS, prefix="b1_u8_"))
         return res
@@ -487,11 +494,11 @@ def main():
         # the reference to pin it
         config["parity"] = "partially pinned: aggregator parity unpinned"
     line = {
-        "metric": f"depth FPS (images/s) at {S}x{S} fp16, {wl.label}, MI355X",
+        "metric": f"depth FPS (images/s) at {S}x{S} {wl.precision}, {wl.label}, MI355X",
         "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": scaling,
         "vs_baseline": None, "throughput_vs_ref_b1": round(value / wl.ref_fps, 3),
-        "dtype": "fp16", "data": "synthetic",
+        "dtype": wl.precision, "data": "synthetic",
         "config": config,
         "rank_seconds": per_rank,
         "model_gflop_per_image": round(wl.gflop, 2),

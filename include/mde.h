@@ -203,6 +203,20 @@ size_t mde_op_attention_ws_bytes(int batch, int heads, int tokens);
 int mde_op_attention_cfg(const void* q_f16, const void* k_f16, const void* vt_f16, void* o_f16, int batch, int heads,
                          int tokens, int tokens_pad, int ldo, const char* cfg, void* ws, size_t ws_bytes,
                          void* stream);
+/* Exact-fp32 kernels of precision "fp32" engines (fp32.hip; v_mfma_f32_16x16x4_f32 /
+ * v_mfma_f32_32x32x2_f32, fp32 operands and accumulation): weights fp32 [Npad][ldw] (ldw % 32 == 0,
+ * zero padded, Npad a multiple of 128), activations fp32 with lda % 4 == 0.  linear32: out = act(a w^T
+ * + bias); linear_residual32: x32 += layer_scale * (a w^T + bias); qkv32: q (times q_scale) / k / v
+ * fp32 [batch*heads][tokens_pad][64]; attention32: softmax over those (q pre-scaled by dh^-0.5 *
+ * log2 e) -> o fp32 [batch*tokens][ldo]. */
+int mde_op_linear32(const float* a, int lda, const float* w, int ldw, int m, int n, int k, const float* bias, int act,
+                    float* out, int ldo, void* stream);
+int mde_op_linear_residual32(const float* a, int lda, const float* w, int ldw, int m, int n, int k,
+                             const float* bias, const float* layer_scale, float* x32, int ldx, void* stream);
+int mde_op_qkv32(const float* a, const float* w, int ldw, const float* bias, int batch, int tokens, int heads,
+                 int tokens_pad, float q_scale, float* q, float* k, float* v, void* stream);
+int mde_op_attention32(const float* q, const float* k, const float* v, float* o, int batch, int heads, int tokens,
+                       int tokens_pad, int ldo, void* stream);
 int mde_op_patch_embed(const float* img, int batch, int h, int w, const void* w_f16, int ldw, const float* bias,
                        const float* pos_patch, const float* cls_pos, int dim, void* patch_scratch_f16,
                        float* x32, void* stream);

@@ -103,6 +103,13 @@ PROTOTYPES = {
     "mde_op_attention_cfg": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_char_p,
                              c_void_p, c_size_t, c_void_p],
     "mde_op_attention": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "mde_op_linear32": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_int,
+                        c_void_p],
+    "mde_op_linear_residual32": [c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p,
+                                 c_void_p, c_int, c_void_p],
+    "mde_op_qkv32": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p,
+                     c_void_p, c_void_p],
+    "mde_op_attention32": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
     "mde_op_patch_embed": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                            c_void_p, c_void_p, c_void_p],
     "mde_op_conv3x3": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,

@@ -6,6 +6,8 @@
 //     padded 14->16 so every 8-element K chunk is 16-byte aligned), plus the
 //     cls row of the residual stream (cls + pos[0]) (a6, a7)
 //   * bilinear resize, align_corners=True, NHWC f16 (a17 fusion upsample)
+#include <type_traits>
+
 #include "mde_device.h"
 #include "mde_ops.h"
 
@@ -15,8 +17,8 @@ namespace {
 
 // One wave per row; PER = D/64 elements per lane, lane-strided (coalesced).
 // XT = float (fp32 residual stream) or f16 (f16 stream); statistics in fp32.
-template <int PER, class XT>
-__global__ void __launch_bounds__(256) layernorm_kernel(const XT* __restrict__ x, f16* __restrict__ y,
+template <int PER, class XT, class YT = f16>
+__global__ void __launch_bounds__(256) layernorm_kernel(const XT* __restrict__ x, YT* __restrict__ y,
                                                         const float* __restrict__ g,
                                                         const float* __restrict__ bt, int rows, float eps,
                                                         int T, int skip_cls) {
@@ -46,11 +48,11 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const XT* __restrict__ x
     q += d * d;
   }
   const float rstd = rsqrtf(wave_sum(q) * (1.0f / D) + eps);
-  f16* yr = y + (size_t)orow * D;
+  YT* yr = y + (size_t)orow * D;
 #pragma unroll
   for (int i = 0; i < PER; ++i) {
     const int c = i * 64 + lane;
-    yr[c] = (f16)((v[i] - mean) * rstd * g[c] + bt[c]);
+    yr[c] = (YT)((v[i] - mean) * rstd * g[c] + bt[c]);
   }
 }
 
@@ -121,7 +123,22 @@ __global__ void __launch_bounds__(256) layernorm_h8_kernel(const f16* __restrict
 
 constexpr int PK = 3 * 14 * 16;  // patch row length (K of the patch-embed GEMM)
 
-__global__ void __launch_bounds__(256) patch_prep_kernel(const float* __restrict__ img, f16* __restrict__ P,
+// 8 patch-row values (kx half) -> P: f16x8, or two float4 (exact-fp32 engines)
+template <class PT>
+MDE_DEV void store8(PT* dst, const float (&v)[8]) {
+  if constexpr (std::is_same<PT, float>::value) {
+    reinterpret_cast<float4*>(dst)[0] = make_float4(v[0], v[1], v[2], v[3]);
+    reinterpret_cast<float4*>(dst)[1] = make_float4(v[4], v[5], v[6], v[7]);
+  } else {
+    f16x8 h;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) h[j] = (f16)v[j];
+    *reinterpret_cast<f16x8*>(dst) = h;
+  }
+}
+
+template <class PT>
+__global__ void __launch_bounds__(256) patch_prep_kernel(const float* __restrict__ img, PT* __restrict__ P,
                                                          float* __restrict__ X, const float* __restrict__ cls_pos,
                                                          int B, int H, int W, int ph, int pw, int T, int D,
                                                          f16* __restrict__ Xh, float* __restrict__ lnst,
@@ -149,10 +166,10 @@ __global__ void __launch_bounds__(256) patch_prep_kernel(const float* __restrict
     const int c = r / 28, ky = (r % 28) >> 1, half = r & 1;
     const int py = pi / pw, px = pi - (pi / pw) * pw;
     const float* src = img + (((size_t)b * 3 + c) * H + py * 14 + ky) * W + px * 14 + half * 8;
-    f16x8 v;
+    float v[8];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (half * 8 + j < 14) ? (f16)src[j] : (f16)0.0f;
-    *reinterpret_cast<f16x8*>(P + patch * PK + c * 224 + ky * 16 + half * 8) = v;
+    for (int j = 0; j < 8; ++j) v[j] = (half * 8 + j < 14) ? src[j] : 0.0f;
+    store8(P + patch * PK + c * 224 + ky * 16 + half * 8, v);
     return;
   }
   id -= nchunk;
@@ -181,7 +198,8 @@ struct InNorm {
   float scale, mean[3], stdv[3];
 };
 
-__global__ void __launch_bounds__(256) patch_prep_u8_kernel(const unsigned char* __restrict__ img, f16* __restrict__ P,
+template <class PT>
+__global__ void __launch_bounds__(256) patch_prep_u8_kernel(const unsigned char* __restrict__ img, PT* __restrict__ P,
                                                             float* __restrict__ X, const float* __restrict__ cls_pos,
                                                             int B, int H, int W, int ph, int pw, int T, int D,
                                                             InNorm nrm, f16* __restrict__ Xh, float* __restrict__ lnst,
@@ -198,7 +216,7 @@ __global__ void __launch_bounds__(256) patch_prep_u8_kernel(const unsigned char*
     const int py = pi / pw, px = pi - (pi / pw) * pw;
     const unsigned char* src = img + (((size_t)b * H + py * 14 + ky) * W + px * 14 + half * 8) * 3;
     const int nvalid = half ? 6 : 8;
-    f16x8 v[3];
+    float v[3][8];
 #pragma unroll
     for (int j = 0; j < 8; ++j)
 #pragma unroll
@@ -208,10 +226,10 @@ __global__ void __launch_bounds__(256) patch_prep_u8_kernel(const unsigned char*
           f = __fdiv_rn((float)src[j * 3 + c], nrm.scale);
           f = __fdiv_rn(__fsub_rn(f, nrm.mean[c]), nrm.stdv[c]);
         }
-        v[c][j] = (f16)f;
+        v[c][j] = f;
       }
 #pragma unroll
-    for (int c = 0; c < 3; ++c) *reinterpret_cast<f16x8*>(P + patch * PK + c * 224 + ky * 16 + half * 8) = v[c];
+    for (int c = 0; c < 3; ++c) store8(P + patch * PK + c * 224 + ky * 16 + half * 8, v[c]);
     return;
   }
   id -= nchunk;
@@ -349,20 +367,39 @@ hipError_t launch_layernorm(const float* x, h16* y, const float* g, const float*
   return hipGetLastError();
 }
 
+hipError_t launch_layernorm32(const float* x, float* y, const float* g, const float* b, int rows, int D, float eps,
+                              hipStream_t st) {
+  if (rows <= 0) return hipSuccess;
+  const dim3 grid((rows + 3) / 4), block(256);
+  switch (D) {
+    case 128: hipLaunchKernelGGL((layernorm_kernel<2, float, float>), grid, block, 0, st, x, y, g, b, rows, eps, 1, 0); break;
+    case 256: hipLaunchKernelGGL((layernorm_kernel<4, float, float>), grid, block, 0, st, x, y, g, b, rows, eps, 1, 0); break;
+    case 384: hipLaunchKernelGGL((layernorm_kernel<6, float, float>), grid, block, 0, st, x, y, g, b, rows, eps, 1, 0); break;
+    case 768: hipLaunchKernelGGL((layernorm_kernel<12, float, float>), grid, block, 0, st, x, y, g, b, rows, eps, 1, 0); break;
+    case 1024: hipLaunchKernelGGL((layernorm_kernel<16, float, float>), grid, block, 0, st, x, y, g, b, rows, eps, 1, 0); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_patch_prep(const float* img, h16* P, float* X, const float* cls_pos, int B, int H, int W, int ph,
-                             int pw, int T, int D, hipStream_t st, h16* Xh, float* lnst, const float* cls_st) {
+                             int pw, int T, int D, hipStream_t st, h16* Xh, float* lnst, const float* cls_st, float* P32) {
   if (lnst && (!cls_st || (D & 31))) return hipErrorInvalidValue;
   const long long n = (long long)B * ph * pw * 84 + (long long)B * D + (lnst ? (long long)B * (D / 16) : 0);
   if (n <= 0) return hipSuccess;
-  hipLaunchKernelGGL(patch_prep_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, img,
-                     reinterpret_cast<f16*>(P), X, cls_pos, B, H, W, ph, pw, T, D, reinterpret_cast<f16*>(Xh), lnst,
-                     cls_st);
+  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  if (P32)
+    hipLaunchKernelGGL(patch_prep_kernel<float>, grid, block, 0, st, img, P32, X, cls_pos, B, H, W, ph, pw, T, D,
+                       reinterpret_cast<f16*>(Xh), lnst, cls_st);
+  else
+    hipLaunchKernelGGL(patch_prep_kernel<f16>, grid, block, 0, st, img, reinterpret_cast<f16*>(P), X, cls_pos, B, H,
+                       W, ph, pw, T, D, reinterpret_cast<f16*>(Xh), lnst, cls_st);
   return hipGetLastError();
 }
 
 hipError_t launch_patch_prep_u8(const unsigned char* img, h16* P, float* X, const float* cls_pos, int B, int H, int W,
                                 int ph, int pw, int T, int D, float scale, const float* mean3, const float* std3,
-                                hipStream_t st, h16* Xh, float* lnst, const float* cls_st) {
+                                hipStream_t st, h16* Xh, float* lnst, const float* cls_st, float* P32) {
   if (ph < 1 || pw < 1 || H < ph * 14 || W < pw * 14 || scale == 0.f) return hipErrorInvalidValue;
   if (lnst && (!cls_st || (D & 31) || !(X || Xh))) return hipErrorInvalidValue;
   const long long n = (long long)B * ph * pw * 28 + ((X || Xh) ? (long long)B * D : 0) +
@@ -374,9 +411,13 @@ hipError_t launch_patch_prep_u8(const unsigned char* img, h16* P, float* X, cons
     nrm.mean[c] = mean3[c];
     nrm.stdv[c] = std3[c];
   }
-  hipLaunchKernelGGL(patch_prep_u8_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, img,
-                     reinterpret_cast<f16*>(P), X, cls_pos, B, H, W, ph, pw, T, D, nrm, reinterpret_cast<f16*>(Xh),
-                     lnst, cls_st);
+  const dim3 grid((unsigned)((n + 255) / 256)), block(256);
+  if (P32)
+    hipLaunchKernelGGL(patch_prep_u8_kernel<float>, grid, block, 0, st, img, P32, X, cls_pos, B, H, W, ph, pw, T, D,
+                       nrm, reinterpret_cast<f16*>(Xh), lnst, cls_st);
+  else
+    hipLaunchKernelGGL(patch_prep_u8_kernel<f16>, grid, block, 0, st, img, reinterpret_cast<f16*>(P), X, cls_pos, B,
+                       H, W, ph, pw, T, D, nrm, reinterpret_cast<f16*>(Xh), lnst, cls_st);
   return hipGetLastError();
 }
 

@@ -63,10 +63,14 @@ std::string setup_dav2(mde_engine* e) {
   std::vector<std::string> need = {"patch.w", "patch.b", "pos.patch", "pos.cls", "norm.g", "norm.b",
                                    "rs0.w", "rs0.b", "rs1.w", "rs1.b", "rs3.w", "rs3.b",
                                    "head.c1.w", "head.c1.b", "head.c2.w", "head.c2.b", "head.c3.w", "head.c3.b"};
-  for (int i = 0; i < c.depth; ++i)
-    for (const char* s : {"ln1.g", "ln1.b", "qkv.w", "qkv.b", "proj.w", "proj.b", "ls1", "ln2.g", "ln2.b",
-                          "fc1.w", "fc1.b", "fc2.w", "fc2.b", "ls2"})
+  if (c.enc_f32 != 0 && c.enc_f32 != 1) return "bad encoder precision in packed config";
+  if (c.enc_f32) need[0] = "patch.w32";
+  const char* wsuf = c.enc_f32 ? ".w32" : ".w";  // exact-fp32 encoders carry fp32 linears
+  for (int i = 0; i < c.depth; ++i) {
+    for (const char* s : {"ln1.g", "ln1.b", "qkv.b", "proj.b", "ls1", "ln2.g", "ln2.b", "fc1.b", "fc2.b", "ls2"})
       need.push_back("b" + std::to_string(i) + "." + s);
+    for (const char* s : {"qkv", "proj", "fc1", "fc2"}) need.push_back("b" + std::to_string(i) + "." + s + wsuf);
+  }
   for (int i = 0; i < 4; ++i) {
     need.push_back("proj" + std::to_string(i) + ".w");
     need.push_back("proj" + std::to_string(i) + ".b");
@@ -169,27 +173,43 @@ size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
                s4 = (size_t)e.h4 * e.w4;
   const size_t s0 = (size_t)(8 * e.ph) * (8 * e.pw);
   DAV2Buf t{};
-  t.P = a.h(bb * np * 672);
+  if (e.cfg.enc_f32) {
+    // exact-fp32 encoder (fp32.hip): fp32 operands end to end; the f16
+    // encoder scratch is not needed, the taps / DPT head below are shared
+    const size_t rows = bb * e.T;
+    t.X = a.f(rows * D);
+    t.P32 = a.f(bb * np * 672);
+    t.Hn32 = a.f(rows * D);
+    t.Q32 = a.f(bb * e.H * e.Tpad * 64);
+    t.K32 = a.f(bb * e.H * e.Tpad * 64);
+    t.V32 = a.f(bb * e.H * e.Tpad * 64);
+    t.O32 = a.f(rows * D);
+    t.Mh32 = a.f(rows * e.cfg.mlp_hidden);
+  }
+  t.P = e.cfg.enc_f32 ? nullptr : a.h(bb * np * 672);
   // residual stream in f16 (precision "fp16": the fp32 update rounded once
   // per residual add, as an fp16 TensorRT engine computes it -- half the
   // bytes of every residual read-modify-write and LayerNorm read) or fp32
-  if (e.cfg.resid_f16) {
+  if (e.cfg.enc_f32) {
+    t.Xh = nullptr;
+  } else if (e.cfg.resid_f16) {
     t.X = nullptr;
     t.Xh = a.h(bb * e.T * D);
   } else {
     t.X = a.f(bb * e.T * D);
     t.Xh = nullptr;
   }
-  t.Hn = a.h(bb * e.T * D);
+  const bool h16enc = !e.cfg.enc_f32;  // the f16 encoder's scratch
+  t.Hn = h16enc ? a.h(bb * e.T * D) : nullptr;
   // LayerNorm folded into qkv / fc1 (packs with the folded weights): the
   // residual writers leave per-32-column (sum, sum of squares) partials here
-  const bool fold = e.cfg.resid_f16 && D % 128 == 0 && D <= 1024 && e.get("pos.cls.st") && !lnfold_off();
+  const bool fold = h16enc && e.cfg.resid_f16 && D % 128 == 0 && D <= 1024 && e.get("pos.cls.st") && !lnfold_off();
   t.st = fold ? a.f(bb * e.T * (D / 16)) : nullptr;
-  t.Q = a.h(bb * e.H * e.Tpad * 64);
-  t.K = a.h(bb * e.H * e.Tpad * 64);
-  t.Vt = a.h(bb * e.H * e.Tpad * 64);
-  t.O = a.h(bb * e.T * D);
-  t.Mh = a.h(bb * e.T * e.cfg.mlp_hidden);
+  t.Q = h16enc ? a.h(bb * e.H * e.Tpad * 64) : nullptr;
+  t.K = h16enc ? a.h(bb * e.H * e.Tpad * 64) : nullptr;
+  t.Vt = h16enc ? a.h(bb * e.H * e.Tpad * 64) : nullptr;
+  t.O = h16enc ? a.h(bb * e.T * D) : nullptr;
+  t.Mh = h16enc ? a.h(bb * e.T * e.cfg.mlp_hidden) : nullptr;
   // tap token maps: only without the tap-LayerNorm fold (the projects read
   // the residual stream directly when proj*.wf is packed)
   const bool fold_taps = fold && e.get("proj0.wf");
@@ -208,11 +228,11 @@ size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
   t.p3 = a.h(bb * s2 * F);
   t.p2 = a.h(bb * s1 * F);
   t.c1 = a.h(bb * s0 * (F / 2));
-  t.ws = bb * e.T <= 4096 ? a.f(4 * bb * e.T * D) : nullptr;
+  t.ws = h16enc && bb * e.T <= 4096 ? a.f(4 * bb * e.T * D) : nullptr;
   // attention split-KV workspace for the batches whose (head, 128-query)
   // grid is under one workgroup per CU (launch_attention splits those)
   const int bsplit = std::min<int>(B, (256 + ((e.T + 127) / 128) * e.H - 1) / (((e.T + 127) / 128) * e.H));
-  t.aws_bytes = bsplit >= 1 ? attention_split_ws_bytes(bsplit, e.H, e.T) : 0;
+  t.aws_bytes = h16enc && bsplit >= 1 ? attention_split_ws_bytes(bsplit, e.H, e.T) : 0;
   t.aws = t.aws_bytes ? a.f(t.aws_bytes / sizeof(float)) : nullptr;
   t.sws = a.f(kSplitWsFloats);
   if (b) *b = t;
@@ -265,6 +285,7 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
   const bool fold = b.st != nullptr;
   split_ws = b.sws;
   const float* cls_st = fold ? w32("pos.cls.st") : nullptr;
+  if (!cf.enc_f32) {
   step("patch_prep", [&] {
     if (cf.input_u8)
       return launch_patch_prep_u8((const unsigned char*)img, b.P, b.Xh ? nullptr : b.X, w32("pos.cls"), B, cf.img_h,
@@ -290,6 +311,7 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
     }
     gemm("patch_embed", g);
   }
+  }  // !enc_f32
   // ---- DPT head: reassemble (project, resize layer) + layerN_rn of tap i ----
   const int hs[4] = {4 * e.ph, 2 * e.ph, e.ph, e.h4};
   const int ws[4] = {4 * e.pw, 2 * e.pw, e.pw, e.w4};
@@ -361,6 +383,88 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
     gemm(nm, g);
   };
   int tap = 0;
+  if (cf.enc_f32) {
+    // ---- exact-fp32 encoder (fp32.hip): every encoder operand fp32, the taps'
+    // final LayerNorm writes the f16 NHWC token maps the DPT head reads ----
+    step("patch_prep", [&] {
+      if (cf.input_u8)
+        return launch_patch_prep_u8((const unsigned char*)img, nullptr, b.X, w32("pos.cls"), B, cf.img_h, cf.img_w,
+                                    e.ph, e.pw, T, D, cf.in_scale, cf.in_mean, cf.in_std, st, nullptr, nullptr,
+                                    nullptr, b.P32);
+      return launch_patch_prep((const float*)img, nullptr, b.X, w32("pos.cls"), B, cf.img_h, cf.img_w, e.ph, e.pw, T,
+                               D, st, nullptr, nullptr, nullptr, b.P32);
+    });
+    {
+      Gemm32Params g = dense32(b.P32, 672, "patch.w32", B * np, D, 672);
+      g.emode = E_PATCH;
+      g.bias = w32("patch.b");
+      g.x32 = b.X;
+      g.ldo = D;
+      g.T = T;
+      g.pos = w32("pos.patch");
+      g.npatch = np;
+      gemm32("patch_embed", g);
+    }
+    for (int i = 0; i < cf.depth; ++i) {
+      const std::string p = "b" + std::to_string(i) + ".";
+      snprintf(nm, sizeof nm, "block%d.norm1", i);
+      step(nm, [&] { return launch_layernorm32(b.X, b.Hn32, w32(p + "ln1.g"), w32(p + "ln1.b"), B * T, D, cf.ln_eps, st); });
+      {
+        Gemm32Params g = dense32(b.Hn32, D, p + "qkv.w32", B * T, 3 * D, D);
+        g.emode = E_QKV;
+        g.bias = w32(p + "qkv.b");
+        g.q = b.Q32;
+        g.k = b.K32;
+        g.v = b.V32;
+        g.T = T;
+        g.Tpad = e.Tpad;
+        g.heads = e.H;
+        g.qscale = 0.125f * 1.4426950408889634f;  // dh^-0.5 * log2(e): scores in log2 units
+        snprintf(nm, sizeof nm, "block%d.qkv", i);
+        gemm32(nm, g);
+      }
+      snprintf(nm, sizeof nm, "block%d.attn", i);
+      step(nm, [&] { return launch_attention32(b.Q32, b.K32, b.V32, b.O32, B, e.H, T, e.Tpad, D, st); });
+      {
+        Gemm32Params g = dense32(b.O32, D, p + "proj.w32", B * T, D, D);
+        g.emode = E_RESID;
+        g.bias = w32(p + "proj.b");
+        g.ls = w32(p + "ls1");
+        g.x32 = b.X;
+        g.ldo = D;
+        snprintf(nm, sizeof nm, "block%d.proj", i);
+        gemm32(nm, g);
+      }
+      snprintf(nm, sizeof nm, "block%d.norm2", i);
+      step(nm, [&] { return launch_layernorm32(b.X, b.Hn32, w32(p + "ln2.g"), w32(p + "ln2.b"), B * T, D, cf.ln_eps, st); });
+      {
+        Gemm32Params g = dense32(b.Hn32, D, p + "fc1.w32", B * T, cf.mlp_hidden, D);
+        g.emode = E_STORE;
+        g.bias = w32(p + "fc1.b");
+        g.act = ACT_GELU;
+        g.out32 = b.Mh32;
+        g.ldo = cf.mlp_hidden;
+        snprintf(nm, sizeof nm, "block%d.fc1", i);
+        gemm32(nm, g);
+      }
+      {
+        Gemm32Params g = dense32(b.Mh32, cf.mlp_hidden, p + "fc2.w32", B * T, D, cf.mlp_hidden);
+        g.emode = E_RESID;
+        g.bias = w32(p + "fc2.b");
+        g.ls = w32(p + "ls2");
+        g.x32 = b.X;
+        g.ldo = D;
+        snprintf(nm, sizeof nm, "block%d.fc2", i);
+        gemm32(nm, g);
+      }
+      if (tap < 4 && cf.taps[tap] == i) {
+        snprintf(nm, sizeof nm, "tap%d.norm", tap);
+        h16* dst = b.tap[tap];
+        step(nm, [&] { return launch_layernorm(b.X, dst, w32("norm.g"), w32("norm.b"), B * T, D, cf.ln_eps, T, 1, st); });
+        ++tap;
+      }
+    }
+  } else {
   for (int i = 0; i < cf.depth; ++i) {
     const std::string p = "b" + std::to_string(i) + ".";
     const std::string pn = "b" + std::to_string(i + 1) + ".";
@@ -476,6 +580,7 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
       ++tap;
     }
   }
+  }  // f16 encoder
   if (tap != 4) return hipErrorInvalidValue;
   for (int i = 0; i < 4; ++i) reassemble(i);
   // ---- fusion (refinenet4 .. refinenet1) ----
@@ -1271,6 +1376,72 @@ int mde_op_attention_cfg(const void* q, const void* k, const void* vt, void* o, 
 
 size_t mde_op_attention_ws_bytes(int batch, int heads, int tokens) {
   return batch > 0 && heads > 0 && tokens > 0 ? attention_split_ws_bytes(batch, heads, tokens) : 0;
+}
+
+int mde_op_linear32(const float* a, int lda, const float* w, int ldw, int m, int n, int k, const float* bias, int act,
+                    float* out, int ldo, void* st) {
+  if (!a || !w || !out) return fail(MDE_ERR_ARG, "null argument");
+  Gemm32Params g;
+  g.A = a;
+  g.lda = lda;
+  g.W = w;
+  g.ldw = ldw;
+  g.M = m;
+  g.N = n;
+  g.K = k;
+  g.bias = bias;
+  g.act = act;
+  g.out32 = out;
+  g.ldo = ldo;
+  OP_RET(launch_gemm32(g, (hipStream_t)st), "linear32");
+}
+
+int mde_op_linear_residual32(const float* a, int lda, const float* w, int ldw, int m, int n, int k,
+                             const float* bias, const float* ls, float* x32, int ldx, void* st) {
+  if (!a || !w || !ls || !x32) return fail(MDE_ERR_ARG, "null argument");
+  Gemm32Params g;
+  g.emode = E_RESID;
+  g.A = a;
+  g.lda = lda;
+  g.W = w;
+  g.ldw = ldw;
+  g.M = m;
+  g.N = n;
+  g.K = k;
+  g.bias = bias;
+  g.ls = ls;
+  g.x32 = x32;
+  g.ldo = ldx;
+  OP_RET(launch_gemm32(g, (hipStream_t)st), "linear_residual32");
+}
+
+int mde_op_qkv32(const float* a, const float* w, int ldw, const float* bias, int batch, int tokens, int heads,
+                 int tokens_pad, float q_scale, float* q, float* k, float* v, void* st) {
+  if (!a || !w || !q || !k || !v) return fail(MDE_ERR_ARG, "null argument");
+  Gemm32Params g;
+  g.emode = E_QKV;
+  g.A = a;
+  g.lda = heads * 64;
+  g.W = w;
+  g.ldw = ldw;
+  g.M = batch * tokens;
+  g.N = 3 * heads * 64;
+  g.K = heads * 64;
+  g.bias = bias;
+  g.q = q;
+  g.k = k;
+  g.v = v;
+  g.T = tokens;
+  g.Tpad = tokens_pad;
+  g.heads = heads;
+  g.qscale = q_scale;
+  OP_RET(launch_gemm32(g, (hipStream_t)st), "qkv32");
+}
+
+int mde_op_attention32(const float* q, const float* k, const float* v, float* o, int batch, int heads, int tokens,
+                       int tokens_pad, int ldo, void* st) {
+  if (!q || !k || !v || !o) return fail(MDE_ERR_ARG, "null argument");
+  OP_RET(launch_attention32(q, k, v, o, batch, heads, tokens, tokens_pad, ldo, (hipStream_t)st), "attention32");
 }
 
 int mde_op_patch_embed(const float* img, int batch, int h, int w, const void* wt, int ldw, const float* bias,

@@ -40,6 +40,9 @@ struct DAV2Buf {
   size_t aws_bytes;
   float* st;        // folded-LN partials [B*T][D/32][2] (f16 residual + folded pack, else null)
   float* sws;       // E_STORE split-K partials (GemmParams::partial_cap = kSplitWsFloats)
+  // exact-fp32 encoder (PackConfig::enc_f32, fp32.hip): fp32 patch rows, LN
+  // output, q / k / v [B*H][Tpad][64], attention output, MLP hidden (else null)
+  float *P32, *Hn32, *Q32, *K32, *V32, *O32, *Mh32;
 };
 
 // fp32 elements of a context's E_STORE split-K workspace (launch_gemm bounds
@@ -270,6 +273,22 @@ struct Runner {
 
   // E_STORE split-K workspace for launch_gemm's small-grid policy (null: never split)
   float* split_ws = nullptr;
+
+  // exact-fp32 dense GEMM (fp32.hip) over fp32 weights [Npad][ldw]
+  Gemm32Params dense32(const float* A, int lda, const std::string& w, int M, int N, int K) {
+    Gemm32Params g;
+    g.A = A;
+    g.lda = lda;
+    g.W = w32(w);
+    g.ldw = ldw(w);
+    g.M = M;
+    g.N = N;
+    g.K = K;
+    return g;
+  }
+  void gemm32(const char* name, const Gemm32Params& g) {
+    step(name, [&] { return launch_gemm32(g, st); });
+  }
 
   void gemm(const char* name, const GemmParams& g) {
     GemmParams q = g;

@@ -90,6 +90,30 @@ struct GemmParams {
   int a_tok = 0;
 };
 
+// Exact-fp32 encoder GEMM (fp32.hip; precision "fp32" engines): C = A W^T
+// with fp32 A [M][lda] (lda % 4 == 0, 16-B aligned) and fp32 W [Npad][ldw]
+// (ldw % 32 == 0, zero-padded), v_mfma_f32_16x16x4_f32.  emode:
+//   E_STORE  out32 (fp32) or out16 (f16) [m*ldo + n] = act(acc + bias)
+//   E_QKV    q (scaled by qscale) / k / v fp32 [B*heads][Tpad][64] rows
+//   E_RESID  x32[m*ldo + n] += ls[n] * (acc + bias[n])
+//   E_PATCH  x32[(b*T + 1 + p)*ldo + n] = acc + bias[n] + pos[p*ldo + n]
+struct Gemm32Params {
+  int emode = E_STORE;
+  int M = 0, N = 0, K = 0;
+  const float* A = nullptr; int lda = 0;
+  const float* W = nullptr; int ldw = 0;
+  const float* bias = nullptr; int act = ACT_NONE;
+  float* out32 = nullptr; h16* out16 = nullptr; int ldo = 0;
+  float* x32 = nullptr; const float* ls = nullptr;
+  float *q = nullptr, *k = nullptr, *v = nullptr; int T = 0, Tpad = 0, heads = 0; float qscale = 1.f;
+  const float* pos = nullptr; int npatch = 0;
+};
+hipError_t launch_gemm32(const Gemm32Params& p, hipStream_t st);
+// fp32 attention over q (pre-scaled by dh^-0.5 * log2 e) / k / v fp32
+// [B*H][Tpad][64] rows -> o fp32 [B*T][ldo], head h in columns 64h .. 64h+63
+hipError_t launch_attention32(const float* q, const float* k, const float* v, float* o, int B, int H, int T,
+                              int Tpad, int ldo, hipStream_t st);
+
 // x32[m*ldo+n] += ls[n] * (sum_{s<S} P[s][m][n] + bias[n]), slices summed in
 // order (elementwise.hip): the second half of the E_RESID split-K path
 hipError_t launch_splitk_resid(const float* P, int S, int M, int N, const float* bias, const float* ls, float* x32,
@@ -127,15 +151,19 @@ size_t attention_split_ws_bytes(int B, int H, int T);
 hipError_t launch_layernorm(const float* x, h16* y, const float* g, const float* b, int rows, int D,
                             float eps, int T, int skip_cls, hipStream_t st, const h16* xh = nullptr);
 
+// P32 (exact-fp32 engines): the patch rows as fp32 into P32 instead of f16 into P
 hipError_t launch_patch_prep_u8(const unsigned char* img, h16* P, float* X, const float* cls_pos, int B, int H, int W,
                                 int ph, int pw, int T, int D, float scale, const float* mean3, const float* std3,
                                 hipStream_t st, h16* Xh = nullptr, float* lnst = nullptr,
-                                const float* cls_st = nullptr);
+                                const float* cls_st = nullptr, float* P32 = nullptr);
 hipError_t launch_depth_postprocess(const float* in, int B, int ih, int iw, float* out, int oh, int ow, float lo,
                                     float hi, hipStream_t st);
 hipError_t launch_patch_prep(const float* img, h16* P, float* X, const float* cls_pos, int B, int H,
                              int W, int ph, int pw, int T, int D, hipStream_t st, h16* Xh = nullptr,
-                             float* lnst = nullptr, const float* cls_st = nullptr);
+                             float* lnst = nullptr, const float* cls_st = nullptr, float* P32 = nullptr);
+// fp32 rows -> LayerNorm -> fp32 rows (exact-fp32 engines)
+hipError_t launch_layernorm32(const float* x, float* y, const float* g, const float* b, int rows, int D, float eps,
+                              hipStream_t st);
 
 hipError_t launch_resize(const h16* in, h16* out, int B, int ih, int iw, int C, int oh, int ow,
                          hipStream_t st);

@@ -51,7 +51,11 @@ struct PackConfig {
   // stream kept in f16 as an fp16 TensorRT engine computes it; 0 = "fp32",
   // fp32 stream (Depth Pro / VGGT: always 0)
   int32_t resid_f16;
-  char reserved[56];
+  // DA-V2: 1 = exact-fp32 encoder (precision "fp32"): fp32 weights *.w32 for
+  // the patch embed and the block linears, fp32 activations, fp32 MFMA
+  // (fp32.hip); 0 = f16 MFMA operands
+  int32_t enc_f32;
+  char reserved[52];
 };
 static_assert(sizeof(PackConfig) == 256, "PackConfig");
 

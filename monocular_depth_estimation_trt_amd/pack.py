@@ -49,6 +49,15 @@ def _pad2(a: np.ndarray, n_mult: int = 128, k_mult: int = 64) -> np.ndarray:
     return out
 
 
+def _pad2_f32(a: np.ndarray, n_mult: int = 128, k_mult: int = 32) -> np.ndarray:
+    """fp32 [Npad][Kpad] (N -> x128, K -> x32, zero padded): the exact-fp32
+    GEMM's weight operand (csrc/fp32.hip)."""
+    n, k = a.shape
+    out = np.zeros((-(-n // n_mult) * n_mult, -(-k // k_mult) * k_mult), np.float32)
+    out[:n, :k] = np.asarray(a, np.float32)
+    return out
+
+
 def _conv3(w: np.ndarray, cin_pad: int = 0) -> np.ndarray:
     """[Cout][Cin][3][3] -> f16 [Cout_pad][9*Cin' pad64] in (ky, kx, ci) order,
     Cin' = cin_pad (zero input channels appended) when given."""
@@ -123,11 +132,12 @@ def _slice_partials(v: np.ndarray) -> np.ndarray:
 
 
 def packed_tensors(sd: Dict[str, np.ndarray], cfg: dict, img_h: int, img_w: int,
-                   fold_ln: bool = False) -> "OrderedDict[str, np.ndarray]":
+                   fold_ln: bool = False, enc_f32: bool = False) -> "OrderedDict[str, np.ndarray]":
     """The packed tensors (name -> f16/f32 numpy array) for one input size.
     fold_ln (precision "fp16" engines) adds the LayerNorm-folded qkv / fc1 /
     DPT project weights (`*.wf`, `*.c1`, `*.c2`) and the cls row's partials
-    (`pos.cls.st`)."""
+    (`pos.cls.st`).  enc_f32 (precision "fp32" engines) stores the patch
+    embed and the block linears as fp32 (`*.w32`) in place of f16."""
     sd = normalize_keys(sd)
     missing = [k for k in W.expected_keys(cfg) if k not in sd and not k.endswith("mask_token")]
     if missing:
@@ -143,7 +153,10 @@ def packed_tensors(sd: Dict[str, np.ndarray], cfg: dict, img_h: int, img_w: int,
     pe = sd[p + "patch_embed.proj.weight"]                   # [D,3,14,14]
     pe16 = np.zeros((D, 3, 14, 16), np.float32)
     pe16[..., :14] = pe
-    o["patch.w"] = _pad2(pe16.reshape(D, 3 * 14 * 16))
+    if enc_f32:
+        o["patch.w32"] = _pad2_f32(pe16.reshape(D, 3 * 14 * 16))
+    else:
+        o["patch.w"] = _pad2(pe16.reshape(D, 3 * 14 * 16))
     o["patch.b"] = f32(sd[p + "patch_embed.proj.bias"])
     pos = interpolate_pos_embed(sd[p + "pos_embed"], ph, pw)
     o["pos.patch"] = np.ascontiguousarray(pos[0, 1:], dtype=np.float32)
@@ -155,21 +168,23 @@ def packed_tensors(sd: Dict[str, np.ndarray], cfg: dict, img_h: int, img_w: int,
         q = f"b{i}."
         o[q + "ln1.g"] = f32(sd[b + "norm1.weight"])
         o[q + "ln1.b"] = f32(sd[b + "norm1.bias"])
-        o[q + "qkv.w"] = _pad2(sd[b + "attn.qkv.weight"])
+        lin = (lambda a: _pad2_f32(a)) if enc_f32 else _pad2  # noqa: E731
+        wsuf = ".w32" if enc_f32 else ".w"
+        o[q + "qkv" + wsuf] = lin(sd[b + "attn.qkv.weight"])
         o[q + "qkv.b"] = f32(sd[b + "attn.qkv.bias"])
-        o[q + "proj.w"] = _pad2(sd[b + "attn.proj.weight"])
+        o[q + "proj" + wsuf] = lin(sd[b + "attn.proj.weight"])
         o[q + "proj.b"] = f32(sd[b + "attn.proj.bias"])
         o[q + "ls1"] = f32(sd[b + "ls1.gamma"])
         o[q + "ln2.g"] = f32(sd[b + "norm2.weight"])
         o[q + "ln2.b"] = f32(sd[b + "norm2.bias"])
-        o[q + "fc1.w"] = _pad2(sd[b + "mlp.fc1.weight"])
+        o[q + "fc1" + wsuf] = lin(sd[b + "mlp.fc1.weight"])
         o[q + "fc1.b"] = f32(sd[b + "mlp.fc1.bias"])
         if fold_ln:
             o[q + "qkv.wf"], o[q + "qkv.c1"], o[q + "qkv.c2"] = _fold_ln(
                 sd[b + "attn.qkv.weight"], sd[b + "attn.qkv.bias"], sd[b + "norm1.weight"], sd[b + "norm1.bias"])
             o[q + "fc1.wf"], o[q + "fc1.c1"], o[q + "fc1.c2"] = _fold_ln(
                 sd[b + "mlp.fc1.weight"], sd[b + "mlp.fc1.bias"], sd[b + "norm2.weight"], sd[b + "norm2.bias"])
-        o[q + "fc2.w"] = _pad2(sd[b + "mlp.fc2.weight"])
+        o[q + "fc2" + wsuf] = lin(sd[b + "mlp.fc2.weight"])
         o[q + "fc2.b"] = f32(sd[b + "mlp.fc2.bias"])
         o[q + "ls2"] = f32(sd[b + "ls2.gamma"])
     o["norm.g"] = f32(sd[p + "norm.weight"])
@@ -225,7 +240,9 @@ def _config_bytes(cfg: dict, img_h: int, img_w: int, input_format: str = "float3
     preamble constants of the reference's add_uint8_input
     (core/onnx_tools.py:87-219): ((u8 / scale) - mean) / std, fp32.
     precision "fp16" keeps the residual stream in f16 (resid_f16 = 1, the
-    reference's fp16 TensorRT engine), "fp32" in fp32."""
+    reference's fp16 TensorRT engine); "fp32" (the reference's default) runs
+    the encoder exactly in fp32 (enc_f32 = 1: fp32 weights, activations and
+    MFMA, csrc/fp32.hip)."""
     if precision not in PRECISIONS:
         raise ValueError(f"precision must be one of {PRECISIONS}, got {precision!r}")
     if input_format not in INPUT_FORMATS:
@@ -244,7 +261,8 @@ def _config_bytes(cfg: dict, img_h: int, img_w: int, input_format: str = "float3
                      *([float(v) for v in std] if u8 else [0.0] * 3))
     assert len(b) == 128, len(b)
     b += b"\0" * 68 + struct.pack("<i", 1 if precision == "fp16" else 0)   # resid_f16 at byte 196
-    return b + b"\0" * 56
+    b += struct.pack("<i", 1 if precision == "fp32" else 0)                 # enc_f32 at byte 200
+    return b + b"\0" * 52
 
 
 def container(tens: "OrderedDict[str, np.ndarray]", cfg_bytes: bytes) -> bytes:
@@ -274,7 +292,7 @@ def container(tens: "OrderedDict[str, np.ndarray]", cfg_bytes: bytes) -> bytes:
 
 def pack_bytes(sd: Dict[str, np.ndarray], cfg: dict, img_h: int = 518, img_w: int = 518,
                input_format: str = "float32_nchw", precision: str = "fp16") -> bytes:
-    return container(packed_tensors(sd, cfg, img_h, img_w, fold_ln=precision == "fp16"),
+    return container(packed_tensors(sd, cfg, img_h, img_w, fold_ln=precision == "fp16", enc_f32=precision == "fp32"),
                      _config_bytes(cfg, img_h, img_w, input_format, precision=precision))
 
 

@@ -81,8 +81,28 @@ def test_precision_sets_residual_stream(stub_load):
             common.get_engine("synthetic:vits", eng, prec, input_hw=(70, 70))
             blob = open(eng, "rb").read(32 + 256)
             assert struct.unpack_from("<i", blob, 32 + 196)[0] == flag, prec
+            # byte 200: enc_f32 -- the exact-fp32 encoder of precision "fp32" (fp32.hip)
+            assert struct.unpack_from("<i", blob, 32 + 200)[0] == (1 if prec == "fp32" else 0), prec
         common.get_engine("synthetic:vits", os.path.join(td, "d.mdeng"), input_hw=(70, 70))   # default: fp32
         assert struct.unpack_from("<i", open(os.path.join(td, "d.mdeng"), "rb").read(288), 228)[0] == 0
+
+
+def test_fp32_pack_carries_fp32_encoder_weights():
+    """precision "fp32" packs the patch embed and every block linear as fp32
+    [Npad][Kpad32] (`*.w32`, the exact-fp32 GEMM's operand) and no f16 copy."""
+    import numpy as np
+    from monocular_depth_estimation_trt_amd import pack, weights
+    cfg = weights.model_config("vits", "metric")
+    sd = weights.synthetic_state_dict(cfg, 3)
+    t = pack.packed_tensors(sd, cfg, 70, 70, enc_f32=True)
+    assert t["patch.w32"].dtype == np.float32 and t["patch.w32"].shape == (384, 672)
+    for i in range(cfg["depth"]):
+        for n, shape in (("qkv", (1152, 384)), ("proj", (384, 384)), ("fc1", (1536, 384)), ("fc2", (384, 1536))):
+            a = t[f"b{i}.{n}.w32"]
+            assert a.dtype == np.float32 and a.shape == shape, (i, n, a.shape)
+            assert f"b{i}.{n}.w" not in t
+    w = sd["pretrained.blocks.0.attn.qkv.weight"]
+    assert np.array_equal(t["b0.qkv.w32"][:w.shape[0], :w.shape[1]], w.astype(np.float32))
 
 
 def test_staleness_rules():

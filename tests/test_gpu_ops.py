@@ -571,3 +571,80 @@ def test_linear_lnfold(gpu, m, n, k, act):
     op("mde_op_linear_lnfold", ptr(x.to(gpu)), ptr(part), 1e-6, ptr(wgp), wgp.shape[1], ptr(c1.to(gpu)),
        ptr(c2.to(gpu)), m, n, k, act, ptr(out), n, stream())
     close(out, ref, 1e-2, 1.5e-2, f"linear_lnfold {m}x{n}x{k}")
+
+
+# ---- exact-fp32 kernels (fp32.hip; precision "fp32" engines) -----------------
+# fp32 operands and accumulation on v_mfma_f32_16x16x4_f32 / 32x32x2_f32: the
+# only differences from a float64 reference are fp32 rounding and summation
+# order (K up to 4096: relative error ~1e-6), so the bars are three orders of
+# magnitude tighter than the f16 kernels' (stated per test).
+
+def pad_w32(w, n_mult=128, k_mult=32):
+    n, k = w.shape
+    out = torch.zeros(-(-n // n_mult) * n_mult, -(-k // k_mult) * k_mult, dtype=torch.float32)
+    out[:n, :k] = w
+    return out
+
+
+@pytest.mark.parametrize("m,n,k,act", [(1370, 1152, 384, 0), (2740, 1536, 384, 2), (1370, 384, 1536, 1),
+                                       (43840, 1536, 384, 2), (77, 96, 40, 0)])
+def test_linear32(gpu, m, n, k, act):
+    """mde_op_linear32 vs a float64 torch reference: 64^2 tiles (small grids)
+    and 128^2 tiles (>= 512 of them), K tails (40 = 32 + 8), GELU(erf) / ReLU."""
+    a, w, b = rn(m, k), rn(n, k, scale=k ** -0.5), rn(n, scale=0.1)
+    ref = a.double() @ w.double().T + b.double()
+    ref = F.relu(ref) if act == 1 else (F.gelu(ref) if act == 2 else ref)
+    wp = pad_w32(w).to(gpu)
+    out = torch.empty(m, n, device=gpu)
+    op("mde_op_linear32", ptr(a.to(gpu)), k, ptr(wp), wp.shape[1], m, n, k, ptr(b.to(gpu)), act, ptr(out), n,
+       stream())
+    close(out, ref.float(), 2e-5, 2e-5, f"linear32 {m}x{n}x{k} act{act}")
+
+
+def test_linear_residual32(gpu):
+    m, n, k = 1370, 384, 1536
+    a, w, b = rn(m, k), rn(n, k, scale=k ** -0.5), rn(n, scale=0.1)
+    ls = 0.5 + 0.05 * rn(n)
+    x = rn(m, n) * 1e5  # far past the f16 range: fp32 storage end to end
+    ref = x.double() + ls.double() * (a.double() @ w.double().T + b.double())
+    xg = x.clone().to(gpu)
+    wp = pad_w32(w).to(gpu)
+    op("mde_op_linear_residual32", ptr(a.to(gpu)), k, ptr(wp), wp.shape[1], m, n, k, ptr(b.to(gpu)),
+       ptr(ls.to(gpu)), ptr(xg), n, stream())
+    close(xg, ref.float(), 2e-6, 2e-3, "linear_residual32")
+
+
+@pytest.mark.parametrize("B,T,H", [(2, 50, 6), (1, 1370, 6)])
+def test_qkv32_layout(gpu, B, T, H):
+    """E_QKV of the fp32 GEMM: q (scaled) / k / v as fp32 [B*H][Tpad][64] rows."""
+    D = H * 64
+    Tp = -(-T // 64) * 64
+    a, w, b = rn(B * T, D), rn(3 * D, D, scale=D ** -0.5), rn(3 * D, scale=0.1)
+    y = (a.double() @ w.double().T + b.double()).reshape(B, T, 3, H, 64).permute(2, 0, 3, 1, 4).reshape(3, B * H, T, 64)
+    qs = 0.125 * LOG2E
+    wp = pad_w32(w).to(gpu)
+    q, k, v = (torch.zeros(B * H, Tp, 64, device=gpu) for _ in range(3))
+    op("mde_op_qkv32", ptr(a.to(gpu)), ptr(wp), wp.shape[1], ptr(b.to(gpu)), B, T, H, Tp, qs, ptr(q), ptr(k), ptr(v),
+       stream())
+    close(q[:, :T], (y[0] * qs).float(), 2e-5, 2e-5, "qkv32 q")
+    close(k[:, :T], y[1].float(), 2e-5, 2e-5, "qkv32 k")
+    close(v[:, :T], y[2].float(), 2e-5, 2e-5, "qkv32 v")
+    assert float(q[:, T:].abs().max()) == 0.0 if Tp > T else True
+
+
+@pytest.mark.parametrize("B,H,T", [(1, 6, 1370), (2, 3, 50), (1, 1, 1), (4, 6, 300), (1, 16, 1370), (24, 6, 1370)])
+def test_attention32(gpu, B, H, T):
+    """mde_op_attention32 vs float64 softmax: the key-group form (small grids,
+    4 waves on one 32-query block, merged through LDS) and the 128-query form
+    (B = 24 at 1370: >= 512 workgroups); masked key tails at every T % 32."""
+    Tp = -(-T // 64) * 64
+    q = rn(B * H, T, 64) * 0.125 * 2.0 * LOG2E
+    k = rn(B * H, T, 64) * 2.0
+    v = rn(B * H, T, 64)
+    ref = torch.softmax((q.double() @ k.double().transpose(1, 2)) / LOG2E, dim=-1) @ v.double()
+    ref = ref.reshape(B, H, T, 64).permute(0, 2, 1, 3).reshape(B * T, H * 64)
+    qg, kg, vg = (torch.zeros(B * H, Tp, 64, device=gpu) for _ in range(3))
+    qg[:, :T], kg[:, :T], vg[:, :T] = q.to(gpu), k.to(gpu), v.to(gpu)
+    o = torch.empty(B * T, H * 64, device=gpu)
+    op("mde_op_attention32", ptr(qg), ptr(kg), ptr(vg), ptr(o), B, H, T, Tp, H * 64, stream())
+    close(o, ref.float(), 1e-4, 1e-5, f"attention32 B{B} H{H} T{T}")
