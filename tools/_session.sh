@@ -1,5 +1,5 @@
 set -o pipefail
-O=gpurun_out/r4s4
+O=gpurun_out/r4s5
 mkdir -p $O
-timeout -k 10 600 python -u -m pytest tests/test_gpu_ops.py tests/test_gpu_engine.py -m gpu -v -s --timeout 300 --timeout-method thread -k "fp32" > $O/fp32.log 2>&1 || exit 1
-bash tools/gpu_tasks.sh $O bench:f32:--no-cpu-baseline,--precision,fp32,--batch,8,--steps,5 bench:f32l1:--no-cpu-baseline,--precision,fp32,--batch,1,--encoder,vitl,--steps,5,--no-b1
+timeout -k 10 600 python -u -m pytest tests/test_gpu_engine.py -m gpu -x -v -s --timeout 300 --timeout-method thread -k "mlp_fused or bench_batches" > $O/mlp.log 2>&1 || exit 1
+bash tools/gpu_tasks.sh $O bench:fused:--no-cpu-baseline,--no-b1 env:MDE_MLPFUSE=0 bench:unfused:--no-cpu-baseline,--no-b1 unenv:MDE_MLPFUSE bench:fused2:--no-cpu-baseline,--no-b1
