@@ -71,7 +71,14 @@ MDE_DEV void mlp_wait(int after) {
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(2)))
 mlp_fused_kernel(const MlpParams p) {
   static_assert(MNSLOT - 2 <= 6, "mlp_wait covers six stages in flight");
-  __shared__ __attribute__((aligned(16))) char ring[MNSLOT * MSB];
+  // one LDS object: the ring, then fc1's fold columns (c1) and bias (c2),
+  // staged once -- a global load inside the stage loop would make its
+  // consumer wait out every ring load issued before it (vmcnt counts loads
+  // and LDS-DMA together, in order).  A second __shared__ variable would give
+  // the LDS accesses alias scopes, and the compiler then drains vmcnt before
+  // every ring read (the ring would stop being a pipeline).
+  __shared__ __attribute__((aligned(16))) char ring[MNSLOT * MSB + 2 * MHID * 4];
+  float* const sc12 = reinterpret_cast<float*>(ring + MNSLOT * MSB);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
@@ -126,6 +133,15 @@ mlp_fused_kernel(const MlpParams p) {
     rstd = rsqrtf(m2 * (1.f / MD) + p.eps);
   }
   const float nm = -rstd * mean;
+  for (int i = tid; i < 2 * MHID / 4; i += 512) {
+    const float* src = i < MHID / 4 ? p.c1 + 4 * i : p.c2 + (4 * i - MHID);
+    const float4 v = *reinterpret_cast<const float4*>(src);
+    *reinterpret_cast<float4*>(sc12 + 4 * i) = v;
+  }
+  // (every load above is consumed before the ring's first LDS-DMA is issued,
+  // so the counted waits below see only the ring; the first step's barrier
+  // publishes sc12)
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 
 #pragma unroll
   for (int s = 0; s < MNSLOT - 1; ++s) issue(s);
@@ -167,18 +183,32 @@ mlp_fused_kernel(const MlpParams p) {
     }
     // LayerNorm fold + bias + GELU, rounded to f16 = fc2's A fragments: fragment
     // q holds blocks 2q (elements 0..3) and 2q + 1 (4..7) of this lane's row
-    // (no c1 / c2 load may be hoisted above the fc1 stages)
-    __builtin_amdgcn_sched_barrier(0);
+    // (c1, c2 of columns n = c*64 + 16 b + 4 g read by inline asm: a plain
+    // LDS read here is not proven disjoint from the ring's LDS-DMA and would
+    // get a compiler-inserted vmcnt(0), draining the ring once per chunk)
+    f32x4 c1v[4], c2v[4];
+    {
+      const unsigned la = (unsigned)(uintptr_t)(sc12 + c * MHC + 4 * g);  // LDS offset (low half of the flat address)
+      asm volatile(
+          "ds_read_b128 %0, %8\n\tds_read_b128 %1, %8 offset:64\n\t"
+          "ds_read_b128 %2, %8 offset:128\n\tds_read_b128 %3, %8 offset:192\n\t"
+          "ds_read_b128 %4, %8 offset:6144\n\tds_read_b128 %5, %8 offset:6208\n\t"
+          "ds_read_b128 %6, %8 offset:6272\n\tds_read_b128 %7, %8 offset:6336\n\t"
+          "s_waitcnt lgkmcnt(0)"
+          : "=v"(c1v[0]), "=v"(c1v[1]), "=v"(c1v[2]), "=v"(c1v[3]), "=v"(c2v[0]), "=v"(c2v[1]), "=v"(c2v[2]),
+            "=v"(c2v[3])
+          : "v"(la)
+          : "memory");
+    }
+    static_assert(MHID * 4 == 6144, "c2 offset in the asm above");
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int n = c * MHC + (2 * q + h) * 16 + 4 * g;
-        const float4 c1 = *reinterpret_cast<const float4*>(p.c1 + n);
-        const float4 c2 = *reinterpret_cast<const float4*>(p.c2 + n);
+        const f32x4 c1 = c1v[2 * q + h], c2 = c2v[2 * q + h];
         const f32x4 a = hacc[2 * q + h];
-        const f32x2 lo = gelu_erf2(f32x2{fmaf(rstd, a[0], nm * c1.x) + c2.x, fmaf(rstd, a[1], nm * c1.y) + c2.y});
-        const f32x2 hi = gelu_erf2(f32x2{fmaf(rstd, a[2], nm * c1.z) + c2.z, fmaf(rstd, a[3], nm * c1.w) + c2.w});
+        const f32x2 lo = gelu_erf2(f32x2{fmaf(rstd, a[0], nm * c1[0]) + c2[0], fmaf(rstd, a[1], nm * c1[1]) + c2[1]});
+        const f32x2 hi = gelu_erf2(f32x2{fmaf(rstd, a[2], nm * c1[2]) + c2[2], fmaf(rstd, a[3], nm * c1[3]) + c2[3]});
         hf[q][4 * h] = (f16)lo[0];
         hf[q][4 * h + 1] = (f16)lo[1];
         hf[q][4 * h + 2] = (f16)hi[0];
