@@ -30,6 +30,9 @@
 // output_conv1 0.259 -> 0.221 ms
 #define MDE_UP_BLEND_F16 1
 #endif
+#ifndef MDE_CONV_TALL
+#define MDE_CONV_TALL 0  // 64-channel convs on 16 x 16 pixel tiles of 8 waves (weights staged once per 256 pixels)
+#endif
 #ifndef MDE_CONV_BRES
 #define MDE_CONV_BRES 1  // 32-wide convs with one channel chunk: all 9 weight taps LDS-resident (1: CK 32, 2: + CK 64)
 #endif
@@ -87,16 +90,16 @@ constexpr int TH = 8, TW = 16;
 // 4-wave tiles of the plain (non-upsampling) conv held to 128 registers: the
 // 64-channel RCU conv (CK 64) otherwise allocates 82 VGPRs + 48 AGPRs = three
 // waves per SIMD; at four its 39 KB of LDS still lets four workgroups share a CU
-template <int BN, int WM, int WN, int CK, int S, bool UP, int EM, bool BRES = false>
-__global__ void __launch_bounds__(WM * WN * 64) __attribute__((amdgpu_waves_per_eu(WM * WN == 4 && !UP ? 4 : 1)))
-conv3_kernel(const GemmParams p) {
+template <int BN, int WM, int WN, int CK, int S, bool UP, int EM, bool BRES = false, int TY = TH>
+__global__ void __launch_bounds__(WM * WN * 64)
+    __attribute__((amdgpu_waves_per_eu((WM * WN == 4 || WM * WN == 8) && !UP ? 4 : 1))) conv3_kernel(const GemmParams p) {
   constexpr int NW = WM * WN, NT = NW * 64;
-  constexpr int BM = TH * TW;
+  constexpr int BM = TY * TW;
   constexpr int TM = BM / (WM * 16), TN = BN / (WN * 16);
   static_assert(TM * WM * 16 == BM && TN * WN * 16 == BN, "tile");
   static_assert(EM != E_HEAD || (BN == 32 && WN == 1), "head epilogue");
   constexpr int ROWB = CK * 2, CH = CK / 8, RWP = 64 / CH;  // patch row bytes, chunks, pixels per wave-instr
-  constexpr int PH = (TH - 1) * S + 3, PW = (TW - 1) * S + 3, PHW = PH * PW;
+  constexpr int PH = (TY - 1) * S + 3, PW = (TW - 1) * S + 3, PHW = PH * PW;
   constexpr int PINS = (PHW + RWP - 1) / RWP;                // glds wave-instructions per patch
   constexpr int PPAD = PINS * RWP;
   constexpr int PATCH = PPAD * ROWB;
@@ -114,7 +117,7 @@ conv3_kernel(const GemmParams p) {
   const int wm = wave / WN, wn = wave - (wave / WN) * WN;
 
   const int Ho = p.oh, Wo = p.ow;
-  const int tiles_x = (Wo + TW - 1) / TW, tiles_y = (Ho + TH - 1) / TH;
+  const int tiles_x = (Wo + TW - 1) / TW, tiles_y = (Ho + TY - 1) / TY;
   const int ntn = (p.N + BN - 1) / BN;
   // XCD-aware order (as the GEMM): workgroups are dealt round-robin over the
   // 8 XCDs, so hand each XCD a contiguous run of tiles -- horizontally and
@@ -131,7 +134,7 @@ conv3_kernel(const GemmParams p) {
   const int n0 = tn * BN;
   // source map geometry: UP -> the (ch x cw) map is upsampled to (uh x uw) first
   const int IH = UP ? p.uh : p.ch, IW = UP ? p.uw : p.cw;
-  const int iy0 = ty * TH * S - 1, ix0 = tx * TW * S - 1;
+  const int iy0 = ty * TY * S - 1, ix0 = tx * TW * S - 1;
   const f16* img = reinterpret_cast<const f16*>(p.A) + (size_t)b * p.ch * p.cw * p.cc;
 
   const int lrow = lane / CH;
@@ -311,7 +314,7 @@ conv3_kernel(const GemmParams p) {
   int mrow[TM];
 #pragma unroll
   for (int i = 0; i < TM; ++i) {
-    const int oy = ty * TH + wm * TM + i, ox = tx * TW + (lane & 15);
+    const int oy = ty * TY + wm * TM + i, ox = tx * TW + (lane & 15);
     mrow[i] = (oy < Ho && ox < Wo) ? ((b * Ho + oy) * Wo + ox) : -1;
   }
 #if MDE_EPI_LDS
@@ -319,7 +322,7 @@ conv3_kernel(const GemmParams p) {
   if (!store_tile_lds<EM, TM, TN>(
           p, acc,
           [&](int row) {
-            const int oy = ty * TH + wm * TM + (row >> 4), ox = tx * TW + (row & 15);
+            const int oy = ty * TY + wm * TM + (row >> 4), ox = tx * TW + (row & 15);
             return (oy < Ho && ox < Wo) ? ((b * Ho + oy) * Wo + ox) : -1;
           },
           n0 + wn * TN * 16, lane, smem + wave * (TM * 16) * (TN * 16) * 4))
@@ -327,18 +330,18 @@ conv3_kernel(const GemmParams p) {
     store_tile<EM, TM, TN>(p, acc, mrow, n0 + wn * TN * 16 + (lane >> 4) * 4, lane);
 }
 
-template <int BN, int WM, int WN, int CK, int S, bool UP, int EM>
+template <int BN, int WM, int WN, int CK, int S, bool UP, int EM, int TY = TH>
 hipError_t run_conv(const GemmParams& p, hipStream_t st) {
   const long long blocks =
-      (long long)p.cb * ((p.oh + TH - 1) / TH) * ((p.ow + TW - 1) / TW) * ((p.N + BN - 1) / BN);
+      (long long)p.cb * ((p.oh + TY - 1) / TY) * ((p.ow + TW - 1) / TW) * ((p.N + BN - 1) / BN);
   if (blocks <= 0) return hipSuccess;
   constexpr bool BRES_OK = BN == 32 && (CK == 32 ? MDE_CONV_BRES >= 1 : MDE_CONV_BRES >= 2);
   if (BRES_OK && p.cc == CK)
-    hipLaunchKernelGGL((conv3_kernel<BN, WM, WN, CK, S, UP, EM, BRES_OK>), dim3((unsigned)blocks),
+    hipLaunchKernelGGL((conv3_kernel<BN, WM, WN, CK, S, UP, EM, BRES_OK, TY>), dim3((unsigned)blocks),
                        dim3(WM * WN * 64), 0, st, p);
   else
-    hipLaunchKernelGGL((conv3_kernel<BN, WM, WN, CK, S, UP, EM>), dim3((unsigned)blocks), dim3(WM * WN * 64), 0,
-                       st, p);
+    hipLaunchKernelGGL((conv3_kernel<BN, WM, WN, CK, S, UP, EM, false, TY>), dim3((unsigned)blocks),
+                       dim3(WM * WN * 64), 0, st, p);
   return hipGetLastError();
 }
 
@@ -363,6 +366,10 @@ hipError_t conv_tiles(const GemmParams& p, hipStream_t st) {
       // 0.854 -> 0.826 ms (same box, profiles/r03_v11_*)
       const long long wg64 = (long long)p.cb * ((p.oh + TH - 1) / TH) * ((p.ow + TW - 1) / TW);
       if (!UP && p.N == 64 && conv_narrow_tiles() && wg64 < 256) return run_conv<32, 4, 1, CK, S, UP, EM>(p, st);
+#if MDE_CONV_TALL
+      if constexpr (!UP && S == 1)
+        if (wg64 >= 2048) return run_conv<64, 8, 1, CK, S, UP, EM, 16>(p, st);
+#endif
       return run_conv<64, 4, 1, CK, S, UP, EM>(p, st);
     }
     const long long wg128 = (long long)p.cb * ((p.oh + TH - 1) / TH) * ((p.ow + TW - 1) / TW) * ((p.N + 127) / 128);

@@ -279,7 +279,7 @@ def test_patch_embed(gpu, B, Hh, Ww):
     (2, 19, 19, 64, 64, 1, 1, 1, 0), (1, 37, 37, 64, 64, 1, 0, 0, 2), (1, 37, 37, 384, 384, 2, 0, 0, 0),
     (1, 74, 74, 96, 64, 1, 0, 0, 0), (2, 28, 28, 48, 64, 1, 0, 0, 1), (1, 148, 148, 64, 32, 1, 0, 1, 0),
     (1, 7, 7, 256, 256, 2, 0, 0, 0), (2, 19, 19, 384, 64, 1, 1, 1, 1), (1, 19, 19, 256, 64, 2, 1, 0, 2),
-    (2, 30, 45, 32, 32, 1, 1, 1, 1)])
+    (2, 30, 45, 32, 32, 1, 1, 1, 1), (4, 296, 296, 64, 64, 1, 1, 0, 2)])
 def test_conv3x3(gpu, B, h, w, cin, cout, stride, relu_in, act, nres):
     x = rn(B, cin, h, w)
     wt, b = rn(cout, cin, 3, 3, scale=(9 * cin) ** -0.5), rn(cout, scale=0.02)
