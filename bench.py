@@ -162,11 +162,6 @@ def roofline(cfg, B, size, layer_ms, frames=1, traffic_file=""):
     else:
         from monocular_depth_estimation_trt_amd import flops
         lf = flops.layer_flops(cfg, size, size, B)
-    # the fused MLP launch (csrc/mlp.hip, "blockN.mlp") does the reference's fc1 + fc2
-    for name in layer_ms:
-        if name.endswith(".mlp") and name not in lf:
-            pre = name[:-len(".mlp")]
-            lf[name] = lf.get(pre + ".fc1", 0.0) + lf.get(pre + ".fc2", 0.0)
     cls_ms, cls_fl, cls_n = {}, {}, {}
     for name, ms in layer_ms.items():
         c = flops.layer_class(name)

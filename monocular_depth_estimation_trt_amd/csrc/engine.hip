@@ -539,31 +539,7 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
         return launch_layernorm(b.X, b.Hn, w32(p + "ln2.g"), w32(p + "ln2.b"), B * T, D, cf.ln_eps, T, 0, st, b.Xh);
       });
     }
-    // large batches of the ViT-S f16 engines: fc1 -> GELU -> fc2 as one
-    // launch (mlp.hip), the hidden layer never leaves the CU (B = 48: 2 x 202
-    // MB of HBM traffic per block saved); it reads the norm2 partials proj
-    // left and writes the next block's norm1 partials in their place
-    const bool mlpfuse = fold && knob(KNOB_MLPFUSE) && mlp_fused_supported(D, cf.mlp_hidden) &&
-                         e.get(p + "fc2.wp") && (long long)B * T >= 128LL * 256;
-    if (mlpfuse) {
-      MlpParams m;
-      m.xh = b.Xh;
-      m.M = B * T;
-      m.lnst = b.st;
-      m.lnst_rows = B * T;
-      m.eps = cf.ln_eps;
-      m.w1 = w16(p + "fc1.wf");
-      m.ldw1 = ldw(p + "fc1.wf");
-      m.c1 = w32(p + "fc1.c1");
-      m.c2 = w32(p + "fc1.c2");
-      m.w2 = w16(p + "fc2.wp");
-      m.ldw2 = ldw(p + "fc2.wp");
-      m.b2 = w32(p + "fc2.b");
-      m.ls2 = w32(p + "ls2");
-      snprintf(nm, sizeof nm, "block%d.mlp", i);
-      step(nm, [&] { return launch_mlp_fused(m, st); });
-    }
-    if (!mlpfuse) {
+    {
       GemmParams g = dense(b.Hn, D, p + "fc1.w", B * T, cf.mlp_hidden, D);
       g.emode = E_STORE;
       g.bias = w32(p + "fc1.b");
@@ -574,7 +550,7 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
       snprintf(nm, sizeof nm, "block%d.fc1", i);
       gemm(nm, g);
     }
-    if (!mlpfuse) {
+    {
       GemmParams g = dense(b.Mh, cf.mlp_hidden, p + "fc2.w", B * T, D, cf.mlp_hidden);
       g.emode = E_RESID;
       g.bias = w32(p + "fc2.b");

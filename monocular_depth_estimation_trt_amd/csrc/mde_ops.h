@@ -114,20 +114,6 @@ hipError_t launch_gemm32(const Gemm32Params& p, hipStream_t st);
 hipError_t launch_attention32(const float* q, const float* k, const float* v, float* o, int B, int H, int T,
                               int Tpad, int ldo, hipStream_t st);
 
-// Fused MLP of the f16-residual ViT-S blocks (mlp.hip): xh [M][384] +=
-// ls2 * (fc2(GELU(fc1(LayerNorm(xh)))) + b2) with the LayerNorm folded into
-// fc1 (w1 = fc1.wf [1536][ldw1], c1 / c2 = fc1.c1 / fc1.c2) and read from the
-// partials lnst [12][lnst_rows][2], which the kernel then overwrites with the
-// updated rows' partials; w2 = fc2.wp [384][ldw2] (fc2's K permuted per
-// 32-column block, pack.py).
-struct MlpParams {
-  h16* xh = nullptr; int M = 0;
-  float* lnst = nullptr; int lnst_rows = 0; float eps = 1e-6f;
-  const h16* w1 = nullptr; int ldw1 = 0; const float* c1 = nullptr; const float* c2 = nullptr;
-  const h16* w2 = nullptr; int ldw2 = 0; const float* b2 = nullptr; const float* ls2 = nullptr;
-};
-bool mlp_fused_supported(int D, int hidden);
-hipError_t launch_mlp_fused(const MlpParams& p, hipStream_t st);
 
 // x32[m*ldo+n] += ls[n] * (sum_{s<S} P[s][m][n] + bias[n]), slices summed in
 // order (elementwise.hip): the second half of the E_RESID split-K path

@@ -34,9 +34,6 @@ enum Knob : int {
   // 8 waves on small-grid 128^2 tiles (1: on).
   // test_gemm_small_grid_variants_bit_exact
   KNOB_W8SMALL,
-  // fused fc1 -> GELU -> fc2 for the ViT-S f16 blocks at large batch (1: on).
-  // test_mlp_fused_matches_unfused
-  KNOB_MLPFUSE,
   KNOB_COUNT
 };
 

@@ -122,20 +122,6 @@ def _fold_ln(w: np.ndarray, bias: np.ndarray, g: np.ndarray, beta: np.ndarray):
     return _pad2(wg), c1.astype(np.float32), c2.astype(np.float32)
 
 
-def _perm_k32(w: np.ndarray) -> np.ndarray:
-    """fc2 weight [N][K] with K permuted inside every 32-column block for the
-    fused MLP (csrc/mlp.hip): stored column 8 g + j holds original column
-    4 g + j (j < 4) or 16 + 4 g + (j - 4) (j >= 4) -- the hidden columns a lane
-    of lane group g holds in the fc1 accumulators it feeds to fc2."""
-    n, k = w.shape
-    assert k % 32 == 0, w.shape
-    g = np.arange(4)[:, None]
-    j = np.arange(8)[None, :]
-    src = np.where(j < 4, 4 * g + j, 16 + 4 * g + (j - 4)).reshape(-1)   # new position 8g + j <- src
-    idx = (np.arange(k // 32)[:, None] * 32 + src[None, :]).reshape(-1)
-    return np.ascontiguousarray(np.asarray(w)[:, idx])
-
-
 def _slice_partials(v: np.ndarray) -> np.ndarray:
     """Per 32-column slice, (sum, sum of squared deviations from the slice
     mean) of the f16-rounded row v -- the LayerNorm partials the fold's
@@ -199,9 +185,6 @@ def packed_tensors(sd: Dict[str, np.ndarray], cfg: dict, img_h: int, img_w: int,
             o[q + "fc1.wf"], o[q + "fc1.c1"], o[q + "fc1.c2"] = _fold_ln(
                 sd[b + "mlp.fc1.weight"], sd[b + "mlp.fc1.bias"], sd[b + "norm2.weight"], sd[b + "norm2.bias"])
         o[q + "fc2" + wsuf] = lin(sd[b + "mlp.fc2.weight"])
-        if fold_ln and D == 384 and cfg["mlp_hidden"] == 1536:
-            # the fused MLP's fc2 operand (csrc/mlp.hip, ViT-S f16 engines)
-            o[q + "fc2.wp"] = _pad2(_perm_k32(sd[b + "mlp.fc2.weight"]))
         o[q + "fc2.b"] = f32(sd[b + "mlp.fc2.bias"])
         o[q + "ls2"] = f32(sd[b + "ls2.gamma"])
     o["norm.g"] = f32(sd[p + "norm.weight"])

@@ -237,26 +237,6 @@ def test_engine_518_bench_batches_vs_oracle(gpu, B):
     assert worst <= 0.003 * 20.0, worst
 
 
-def test_mlp_fused_matches_unfused(gpu):
-    """Switch "mlpfuse" (tuning.h): the ViT-S f16 engines' fused fc1 -> GELU ->
-    fc2 (csrc/mlp.hip; taken from B * T >= 32768, here B = 24) against the two
-    GEMMs it replaces and against the oracle.  The hidden layer is rounded to
-    f16 as the unfused fc1 stores it; fc2 sums K in a permuted order (the
-    packer's fc2.wp), so the two engines agree to fp32 reassociation."""
-    cfg = weights.model_config("vits", "metric")
-    sd = weights.synthetic_state_dict(cfg, 2024)
-    x = weights.synthetic_images(24, 518, 518, first_seed=200)
-    blob = pack.pack_bytes(sd, cfg, 518, 518)
-    y_fused = run_engine(blob, x)
-    with _lib.tuning(mlpfuse=0):
-        y_plain = run_engine(blob, x)
-    m = depth_metrics(y_fused, y_plain)
-    print("fused vs unfused MLP", m)
-    assert m["rel_mean"] < 1e-3 and m["corr"] >= CORR and m["max_abs"] < 0.06, m
-    ref = _oracle_chunks(sd, cfg, x)
-    check(y_fused, ref, 20.0, "518 B=24 fused MLP vs oracle")
-
-
 def test_lnfold_matches_layernorm(gpu):
     """Switch "lnfold" = 0 (read at context creation): norm1 / norm2 / the tap
     norms as LayerNorm launches and the unfolded qkv / fc1 / project weights,

@@ -164,21 +164,3 @@ def test_layernorm_fold(small):
     assert "b0.qkv.wf" not in pack.packed_tensors(sd, cfg, 98, 98)
 
 
-def test_fc2_k_permutation_for_the_fused_mlp():
-    """pack._perm_k32 (fc2.wp, csrc/mlp.hip): inside every 32-column block,
-    stored column 8g + j holds original column 4g + j (j < 4) or 16 + 4g +
-    (j - 4) -- the hidden columns lane group g holds in the fc1 accumulators.
-    A bijection per block, so y = h W2^T is unchanged when h is permuted alike."""
-    import numpy as np
-    from monocular_depth_estimation_trt_amd import pack
-    rng = np.random.default_rng(0)
-    w = rng.standard_normal((8, 96)).astype(np.float32)
-    wp = pack._perm_k32(w)
-    for blk in range(3):
-        for g in range(4):
-            for j in range(8):
-                src = 4 * g + j if j < 4 else 16 + 4 * g + (j - 4)
-                assert np.array_equal(wp[:, 32 * blk + 8 * g + j], w[:, 32 * blk + src])
-    h = rng.standard_normal((5, 96)).astype(np.float32)
-    hp = pack._perm_k32(h)
-    assert np.allclose(hp @ wp.T, h @ w.T, rtol=1e-5, atol=1e-5)

@@ -1,3 +1,13 @@
+// EXPERIMENT, not part of libmde_hip (round 4, measured slower; DESIGN.md
+// section 9 "Round 4: the fused MLP").  Built only by tools/mlp_probe.hip,
+// whose synthetic run checks it against a CPU restatement and stamps its
+// phases.  At ViT-S B = 48 the fused launch took 3.80 ms per forward against
+// 3.1 ms for the unfused fc1 + fc2: a workgroup streams all 2.36 MB of the
+// block's MLP weights through L2 -> LDS at ~13 B/clk/CU (1325 clocks per 16 KB
+// stage against 512 MFMA clocks), and 514 workgroups at one per CU take 3
+// rounds.  The weight ring's LDS-DMA is buffer_load ... lds (see mblds below)
+// with its address registers kept live (see ka[] in the kernel).
+//
 // Fused DINOv2 MLP for the f16-residual ViT-S blocks at large batch (gfx950):
 //
 //   x += ls2 * (fc2(GELU(fc1(LN2(x)))) + b2)          
@@ -30,10 +40,26 @@
 // per 16 KB): one workgroup per CU, MFMA- and L2->LDS-bound in about equal
 // measure, where the two unfused GEMMs were bound by their tiles' L2 -> LDS
 // traffic (every 128^2 tile re-reading its A rows) and the hidden round trip.
-#include "mde_device.h"
-#include "mde_ops.h"
+#include "../../monocular_depth_estimation_trt_amd/csrc/mde_device.h"
+#include "../../monocular_depth_estimation_trt_amd/csrc/mde_ops.h"
 
 namespace mde {
+
+// Fused MLP of the f16-residual ViT-S blocks (this file): xh [M][384] +=
+// ls2 * (fc2(GELU(fc1(LayerNorm(xh)))) + b2) with the LayerNorm folded into
+// fc1 (w1 = fc1.wf [1536][ldw1], c1 / c2 = fc1.c1 / fc1.c2) and read from the
+// partials lnst [12][lnst_rows][2], which the kernel then overwrites with the
+// updated rows' partials; w2 = fc2.wp [384][ldw2] (fc2's K permuted per
+// 32-column block, pack.py).
+struct MlpParams {
+  h16* xh = nullptr; int M = 0;
+  float* lnst = nullptr; int lnst_rows = 0; float eps = 1e-6f;
+  const h16* w1 = nullptr; int ldw1 = 0; const float* c1 = nullptr; const float* c2 = nullptr;
+  const h16* w2 = nullptr; int ldw2 = 0; const float* b2 = nullptr; const float* ls2 = nullptr;
+};
+bool mlp_fused_supported(int D, int hidden);
+hipError_t launch_mlp_fused(const MlpParams& p, hipStream_t st);
+
 
 namespace {
 
@@ -46,8 +72,38 @@ constexpr int MNSLOT = 8;
 // hidden columns each)
 constexpr int MSPC = 6;
 constexpr int MNST = MNCH * MSPC;     // 144 stages per pass
+constexpr int MNWV = 8, MROWS = 128;  // waves per workgroup, token rows per workgroup
 
-MDE_DEV void mglds(const void* src, void* lds) { __builtin_amdgcn_global_load_lds(src, lds, 16, 0, 0); }
+// LDS-DMA as buffer_load ... lds (MUBUF), not global_load_lds: hipcc counts a
+// pending FLAT-encoded LDS-DMA as an out-of-order lgkm event, and then every
+// ds_read wait in its shadow becomes lgkmcnt(0) -- no LDS read overlaps an
+// MFMA.  The buffer form keeps the counted lgkmcnt(N) waits.
+typedef __amdgpu_buffer_rsrc_t mrsrc_t;
+MDE_DEV mrsrc_t mrsrc(const void* base) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, 0x7fffffff, 0x00020000);
+}
+#ifndef MLP_GLDS
+#define MLP_GLDS 0  // probe A/B: 1 = the FLAT global_load_lds form
+#endif
+MDE_DEV void mblds(const void* base, mrsrc_t r, unsigned off, void* lds) {
+#if MLP_GLDS
+  (void)r;
+  __builtin_amdgcn_global_load_lds(reinterpret_cast<const char*>(base) + off, lds, 16, 0, 0);
+#else
+  (void)base;
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, off, 0, 0, 0);
+#endif
+}
+
+// timing probe (tools/mlp_probe.hip defines MLP_PROBE 1): per-wave clock
+// stamps of the kernel's phases into g_mlp_probe; compiled out otherwise
+#ifndef MLP_PROBE
+#define MLP_PROBE 0
+#endif
+#if MLP_PROBE
+__device__ unsigned long long* g_mlp_probe;
+#define MLP_CLK() __builtin_amdgcn_s_memtime()
+#endif
 
 MDE_DEV void mlp_barrier() {
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -82,6 +138,11 @@ mlp_fused_kernel(const MlpParams p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4;
+#if MLP_PROBE
+  unsigned long long pt[8], twait = 0;
+  pt[0] = MLP_CLK();
+  pt[7] = __builtin_amdgcn_s_memrealtime();
+#endif
   const int row = blockIdx.x * 128 + wave * 16 + (lane & 15);
   const bool rv = row < p.M;
   const int rr = rv ? row : p.M - 1;
@@ -92,17 +153,21 @@ mlp_fused_kernel(const MlpParams p) {
   // swizzle on the source chunk)
   const int lrow = lane >> 3;
   const int lch = (lane & 7) ^ lrow;
-  const f16* w1 = reinterpret_cast<const f16*>(p.w1);
-  const f16* w2 = reinterpret_cast<const f16*>(p.w2);
+  const mrsrc_t rw1 = mrsrc(p.w1), rw2 = mrsrc(p.w2);
+  // the DMA's address registers are kept live until the next step: reusing
+  // them at once (as ds_read destinations) raced the in-flight LDS-DMA
+  // (nondeterministic outputs; the VGPR read of a VMEM address is not
+  // finished at issue)
+  unsigned ka[2] = {0u, 0u};
   auto issue = [&](int s) {
     const int c = s / MSPC, r = s - (s / MSPC) * MSPC;
     char* slot = ring + (s % MNSLOT) * MSB;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int ins = wave + 8 * i;  // sub-tile i of a W1 stage; rows 64 i + .. of a W2 stage
-      const f16* src = r < 3 ? w1 + (size_t)(c * MHC + wave * 8 + lrow) * p.ldw1 + r * 128 + i * 64
-                             : w2 + (size_t)((r - 3) * 128 + ins * 8 + lrow) * p.ldw2 + c * MHC;
-      mglds(src + lch * 8, slot + ins * 1024);
+      ka[i] = r < 3 ? ((c * MHC + wave * 8 + lrow) * p.ldw1 + r * 128 + i * 64 + lch * 8) * 2
+                    : (((r - 3) * 128 + ins * 8 + lrow) * p.ldw2 + c * MHC + lch * 8) * 2;
+      mblds(r < 3 ? (const void*)p.w1 : (const void*)p.w2, r < 3 ? rw1 : rw2, ka[i], slot + ins * 1024);
     }
   };
 
@@ -142,6 +207,9 @@ mlp_fused_kernel(const MlpParams p) {
   // so the counted waits below see only the ring; the first step's barrier
   // publishes sc12)
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if MLP_PROBE
+  pt[1] = MLP_CLK();
+#endif
 
 #pragma unroll
   for (int s = 0; s < MNSLOT - 1; ++s) issue(s);
@@ -158,8 +226,16 @@ mlp_fused_kernel(const MlpParams p) {
   };
   // one pipeline step: stage s landed and visible, the next refill issued
   auto step_in = [&](int s) -> const char* {
+    asm volatile("" ::"v"(ka[0]), "v"(ka[1]));
+#if MLP_PROBE
+    const unsigned long long ta = MLP_CLK();
+#endif
     mlp_wait(min(MNST - 1 - s, MNSLOT - 2));
     mlp_barrier();  // stage s visible to all; stage s - 1 fully consumed
+#if MLP_PROBE
+    twait += MLP_CLK() - ta;
+    if (s == 0) pt[2] = MLP_CLK();
+#endif
     if (s + MNSLOT - 1 < MNST) issue(s + MNSLOT - 1);
     return ring + (s % MNSLOT) * MSB;
   };
@@ -229,6 +305,9 @@ mlp_fused_kernel(const MlpParams p) {
     }
   }
 
+#if MLP_PROBE
+  pt[3] = MLP_CLK();
+#endif
   // ---- epilogue: x += ls2 * (acc + b2), one rounding; the next LayerNorm's
   // partials per 32-column slice (columns {4g..} of blocks 2q, 2q + 1 across
   // the four lane groups of the row)
@@ -265,6 +344,16 @@ mlp_fused_kernel(const MlpParams p) {
     s2 += __shfl_xor(s2, 32);
     if (g == 0 && rv) *reinterpret_cast<float2*>(p.lnst + ((size_t)q * p.lnst_rows + rr) * 2) = make_float2(s1, s2);
   }
+#if MLP_PROBE
+  pt[4] = MLP_CLK();
+  pt[5] = twait;
+  pt[6] = __builtin_amdgcn_s_memrealtime();
+  if (lane == 0) {
+    unsigned long long* o = g_mlp_probe + ((size_t)blockIdx.x * 8 + wave) * 8;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) o[k] = pt[k];
+  }
+#endif
 }
 
 }  // namespace
