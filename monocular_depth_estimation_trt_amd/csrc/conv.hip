@@ -30,9 +30,6 @@
 // output_conv1 0.259 -> 0.221 ms
 #define MDE_UP_BLEND_F16 1
 #endif
-#ifndef MDE_CONV_TALL
-#define MDE_CONV_TALL 0  // 64-channel convs on 16 x 16 pixel tiles of 8 waves (weights staged once per 256 pixels)
-#endif
 #ifndef MDE_CONV_BRES
 #define MDE_CONV_BRES 1  // 32-wide convs with one channel chunk: all 9 weight taps LDS-resident (1: CK 32, 2: + CK 64)
 #endif
@@ -366,10 +363,6 @@ hipError_t conv_tiles(const GemmParams& p, hipStream_t st) {
       // 0.854 -> 0.826 ms (same box, profiles/r03_v11_*)
       const long long wg64 = (long long)p.cb * ((p.oh + TH - 1) / TH) * ((p.ow + TW - 1) / TW);
       if (!UP && p.N == 64 && conv_narrow_tiles() && wg64 < 256) return run_conv<32, 4, 1, CK, S, UP, EM>(p, st);
-#if MDE_CONV_TALL
-      if constexpr (!UP && S == 1)
-        if (wg64 >= 2048) return run_conv<64, 8, 1, CK, S, UP, EM, 16>(p, st);
-#endif
       return run_conv<64, 4, 1, CK, S, UP, EM>(p, st);
     }
     const long long wg128 = (long long)p.cb * ((p.oh + TH - 1) / TH) * ((p.ow + TW - 1) / TW) * ((p.N + 127) / 128);

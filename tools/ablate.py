@@ -67,11 +67,6 @@ VARIANTS = {
           if (t2 <= 256 && p.M >= 256) return run<256, 128, 4, 2, AM, EM, 32>(p, st);
           return run<128, 128, 2, 4, AM, EM>(p, st);
         }""", 1)]),
-    # candidate (not an ablation): 64-channel S=1 convs on large grids as
-    # 16 x 16 pixel tiles of 8 waves -- the 72 KB weight set staged once per
-    # 256 pixels instead of per 128 (rcu.conv L2 -> LDS fills, VERDICT r3 item 5)
-    "conv_tall": ("conv.hip", [
-        ("#define MDE_CONV_TALL 0", "#define MDE_CONV_TALL 1", 1)]),
     # GEMM main loop only: the epilogue returns unless a NaN appears (r02's
     # MDE_EXP_NOEPI, profiles/r02_v10_epilogue_cost_*)
     "gemm_noepi": ("gemm.hip", [

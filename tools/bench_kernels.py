@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--lib", default="")
     ap.add_argument("--only", default="")
+    ap.add_argument("--attn-cfgs", default="", help="comma list of attention launch configs to time (mde_op_attention_cfg)")
     ap.add_argument("--dim", type=int, default=384, help="ViT width D (ViT-L: 1024)")
     ap.add_argument("--heads", type=int, default=6, help="attention heads (ViT-L: 16)")
     ap.add_argument("--tokens", type=int, default=1370, help="tokens per image (GEMM rows = batch x tokens)")
@@ -100,6 +101,11 @@ def main():
     o = torch.empty(M, D, dtype=torch.float16, device=dev)
     timeit(f"attention T{T} H{H}", lambda: L.mde_op_attention(ptr(q), ptr(k_), ptr(vt), ptr(o), B, H, T, Tp, D, st),
            4.0 * B * H * T * T * 64)
+    ws = torch.empty(64 << 20, dtype=torch.uint8, device=dev)
+    for cfg in [c for c in a.attn_cfgs.replace("+", ",").split(",") if c]:
+        timeit(f"attention T{T} H{H} cfg {cfg}",
+               lambda: L.mde_op_attention_cfg(ptr(q), ptr(k_), ptr(vt), ptr(o), B, H, T, Tp, D, cfg.encode(), ptr(ws),
+                                              ws.numel(), st), 4.0 * B * H * T * T * 64)
     F = 64
     for hw in (148, 74):
         xin = rnd(B, hw, hw, F)
