@@ -417,6 +417,9 @@ def main():
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
+    # one rank per GPU; more ranks than visible GPUs (a rehearsal on a smaller
+    # box) share them round-robin -- device_count() does not initialise HIP
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
 
     from monocular_depth_estimation_trt_amd import replicas
