@@ -237,6 +237,39 @@ def test_engine_518_bench_batches_vs_oracle(gpu, B):
     assert worst <= 0.003 * 20.0, worst
 
 
+def test_engine_b48_replays_bit_identical(gpu):
+    """The bench's graph (ViT-S 518^2, B = 48) replayed three times in one
+    context and once eagerly gives bit-identical maps: every kernel on the
+    path is deterministic (no atomics, fixed split-K / key-group merge
+    orders) and no LDS-DMA races its consumers -- round 4's fused-MLP
+    experiment lost exactly this property to an address-register race
+    (DESIGN.md section 9), so it is checked on the product graph."""
+    cfg = weights.model_config("vits", "metric")
+    sd = weights.synthetic_state_dict(cfg, 1234)
+    B = 48
+    x = weights.synthetic_images(B, 518, 518, first_seed=3)
+    eng = Engine.from_bytes(pack.pack_bytes(sd, cfg, 518, 518), 0,
+                            profile=((1, 3, 518, 518), (B, 3, 518, 518), (B, 3, 518, 518)))
+    ctx = eng.create_execution_context()
+    xin = torch.from_numpy(x).cuda()
+    out = torch.empty(B, 518, 518, device="cuda")
+    ctx.set_input_shape("input", x.shape)
+    ctx.set_tensor_address("input", xin.data_ptr())
+    ctx.set_tensor_address("output", out.data_ptr())
+    ys = []
+    for graph in (True, True, True, False):
+        ctx.set_graph_mode(graph)
+        out.fill_(float("nan"))
+        ctx.execute_async_v3(torch.cuda.current_stream().cuda_stream)
+        torch.cuda.synchronize()
+        ys.append(out.cpu().numpy())
+    ctx.destroy()
+    eng.destroy()
+    assert np.isfinite(ys[0]).all()
+    for i, y in enumerate(ys[1:], 1):
+        assert np.array_equal(y, ys[0]), f"run {i} differs: max {np.abs(y - ys[0]).max()}"
+
+
 def test_lnfold_matches_layernorm(gpu):
     """Switch "lnfold" = 0 (read at context creation): norm1 / norm2 / the tap
     norms as LayerNorm launches and the unfolded qkv / fc1 / project weights,
