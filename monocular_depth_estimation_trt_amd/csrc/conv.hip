@@ -316,7 +316,7 @@ __global__ void __launch_bounds__(WM * WN * 64)
   }
 #if MDE_EPI_LDS
   // the main loop ended on a barrier: the LDS is free
-  if (!store_tile_lds<EM, TM, TN>(
+  if (!store_tile_lds<EM, TM, TN, 0, true>(
           p, acc,
           [&](int row) {
             const int oy = ty * TY + wm * TM + (row >> 4), ox = tx * TW + (row & 15);

@@ -197,7 +197,7 @@ MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&m
 // first output column; the caller has retired every LDS read of the main
 // loop (barrier) before the call.  Returns false (nothing written) for modes
 // it does not stage -- the caller then runs store_tile.
-template <int EM, int TM, int TN, int HALF = 0, class RowMap>
+template <int EM, int TM, int TN, int HALF = 0, bool PRES = false, class RowMap>
 MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mof, int n0w, int lane, char* lds) {
   constexpr int R = TM * 16, C = TN * 16;  // wave tile
   constexpr int CHR = C / 4;               // 16-B fp32 chunks per staged row
@@ -423,8 +423,10 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
       // trip (load -> vmcnt(0) -> store).  A lane reads and writes only its
       // own elements, so loading ahead is safe in place.
       constexpr int IT = (RP + RPI - 1) / RPI;
-      constexpr bool PRE = EM == E_RESID;  // (E_STORE's residuals: +22 VGPRs on the fc1 tile for ~2 % of rcu.conv)
-      f16x8 pre0[PRE ? IT : 1];
+      // (E_STORE's residuals only where the caller asks, PRES: the direct
+      // convs -- on the fc1 GEMM tile the arrays cost 22 VGPRs)
+      constexpr bool PRE = EM == E_RESID || (EM == E_STORE && PRES && !RAW);
+      f16x8 pre0[PRE ? IT : 1], pre1[EM == E_STORE && PRE ? IT : 1];
       if constexpr (PRE) {
 #pragma unroll
         for (int it = 0; it < IT; ++it) {
@@ -433,7 +435,12 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
           const int m = mof(PS * RP + row);
           if (m < 0) continue;
           const size_t o = (size_t)m * p.ldo + n;
-          if (p.xh) pre0[it] = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.xh) + o);
+          if constexpr (EM == E_STORE) {
+            if (p.res0) pre0[it] = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res0) + res0_offset(p, m, n, o));
+            if (p.res1) pre1[it] = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res1) + o);
+          } else {
+            if (p.xh) pre0[it] = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.xh) + o);
+          }
         }
       }
 #pragma unroll
@@ -471,8 +478,9 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
             continue;
           }
           if (p.res0) {
-            const f16x8 r0 =
-                *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res0) + res0_offset(p, m, n, o));
+            f16x8 r0;
+            if constexpr (PRE) r0 = pre0[it];
+            else r0 = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res0) + res0_offset(p, m, n, o));
             if (p.res0_relu) {
 #pragma unroll
               for (int r = 0; r < 8; ++r) v[r] += fmaxf((float)r0[r], 0.f);
@@ -482,7 +490,9 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
             }
           }
           if (p.res1) {
-            const f16x8 r1 = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res1) + o);
+            f16x8 r1;
+            if constexpr (PRE) r1 = pre1[it];
+            else r1 = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res1) + o);
 #pragma unroll
             for (int r = 0; r < 8; ++r) v[r] += (float)r1[r];
           }
