@@ -441,16 +441,30 @@ __global__ void splitk_resid_kernel(const float* __restrict__ P, int S, int M, i
   if (i >= (long long)M * n4) return;  // M * n4 is a multiple of 8 (N % 32 == 0): 8-lane groups stay whole
   const int m = (int)(i / n4), n = (int)(i - (long long)m * n4) * 4;
   const size_t plane = (size_t)M * N;
-  float4 a = *reinterpret_cast<const float4*>(P + (size_t)m * N + n);
-  for (int s = 1; s < S; ++s) {
-    const float4 b = *reinterpret_cast<const float4*>(P + s * plane + (size_t)m * N + n);
-    a.x += b.x; a.y += b.y; a.z += b.z; a.w += b.w;
-  }
+  // every operand loaded up front and the slices four at a time (a runtime
+  // loop of load -> add paid one round trip per slice), summed in order
+  // 0..S-1 as before
   const float4 bn = bias ? *reinterpret_cast<const float4*>(bias + n) : float4{0.f, 0.f, 0.f, 0.f};
   const float4 l = *reinterpret_cast<const float4*>(ls + n);
+  f16x4 xh0{};
+  float4 x320{};
+  if (xh) xh0 = *reinterpret_cast<const f16x4*>(xh + (size_t)m * ldo + n);
+  else x320 = *reinterpret_cast<const float4*>(x32 + (size_t)m * ldo + n);
+  float4 a = *reinterpret_cast<const float4*>(P + (size_t)m * N + n);
+  for (int s0 = 1; s0 < S; s0 += 4) {
+    float4 b[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (s0 + j < S) b[j] = *reinterpret_cast<const float4*>(P + (s0 + j) * plane + (size_t)m * N + n);
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (s0 + j < S) {
+        a.x += b[j].x; a.y += b[j].y; a.z += b[j].z; a.w += b[j].w;
+      }
+  }
   if (xh) {
     f16x4* x = reinterpret_cast<f16x4*>(xh + (size_t)m * ldo + n);
-    f16x4 xv = *x;
+    f16x4 xv = xh0;
     xv[0] = (f16)((float)xv[0] + l.x * (a.x + bn.x));
     xv[1] = (f16)((float)xv[1] + l.y * (a.y + bn.y));
     xv[2] = (f16)((float)xv[2] + l.z * (a.z + bn.z));
@@ -475,7 +489,7 @@ __global__ void splitk_resid_kernel(const float* __restrict__ P, int S, int M, i
     return;
   }
   float4* x = reinterpret_cast<float4*>(x32 + (size_t)m * ldo + n);
-  float4 xv = *x;
+  float4 xv = x320;
   xv.x += l.x * (a.x + bn.x);
   xv.y += l.y * (a.y + bn.y);
   xv.z += l.z * (a.z + bn.z);
@@ -507,11 +521,20 @@ __global__ void splitk_store_kernel(const float* __restrict__ P, int S, int M, i
   const size_t plane = (size_t)M * N;
   const float* src = P + (size_t)m * N + n;
   float4 a0 = *reinterpret_cast<const float4*>(src), a1 = *reinterpret_cast<const float4*>(src + 4);
-  for (int s = 1; s < S; ++s) {
-    const float4 b0 = *reinterpret_cast<const float4*>(src + s * plane);
-    const float4 b1 = *reinterpret_cast<const float4*>(src + s * plane + 4);
-    a0.x += b0.x; a0.y += b0.y; a0.z += b0.z; a0.w += b0.w;
-    a1.x += b1.x; a1.y += b1.y; a1.z += b1.z; a1.w += b1.w;
+  for (int s0 = 1; s0 < S; s0 += 4) {  // four slices per batch of loads, summed in order
+    float4 b0[4], b1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (s0 + j < S) {
+        b0[j] = *reinterpret_cast<const float4*>(src + (s0 + j) * plane);
+        b1[j] = *reinterpret_cast<const float4*>(src + (s0 + j) * plane + 4);
+      }
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (s0 + j < S) {
+        a0.x += b0[j].x; a0.y += b0[j].y; a0.z += b0[j].z; a0.w += b0[j].w;
+        a1.x += b1[j].x; a1.y += b1[j].y; a1.z += b1[j].z; a1.w += b1[j].w;
+      }
   }
   float v[8] = {a0.x, a0.y, a0.z, a0.w, a1.x, a1.y, a1.z, a1.w};
   if (p.bias) {
