@@ -229,7 +229,7 @@ def call(name: str, *args) -> None:
         raise MDEError(name, rc, last_error())
 
 
-TUNING = ("splitk", "lnfold", "conv_narrow", "upconv", "gemm256", "deep64", "w8small")
+TUNING = ("splitk", "lnfold", "conv_narrow", "upconv", "gemm256", "deep64", "w8small", "conv_persist")
 
 
 def get_tuning(name: str) -> int:

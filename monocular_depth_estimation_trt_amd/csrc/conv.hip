@@ -15,6 +15,7 @@
 // with the chunk swizzle of the GEMM (c ^ (pix & 7) for 128-B rows,
 // c ^ ((pix >> 1) & 3) for 64-B rows): conflict-free fragment reads at S = 1.
 #include <cstdlib>
+#include <type_traits>
 
 #include "mde_device.h"
 #include "mde_ops.h"
@@ -44,6 +45,26 @@ MDE_DEV void glds16c(const void* src, void* lds_wave_base) {
   __builtin_amdgcn_global_load_lds(src, lds_wave_base, 16, 0, 0);
 }
 MDE_DEV void wait_vmc() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
+// The same LDS-DMA (64-bit vaddr form) issued from inline asm: hipcc does not
+// see it, so its ds_read waits in the DMA's shadow stay counted (lgkmcnt(N))
+// instead of lgkmcnt(0) -- it models a pending FLAT LDS-DMA as an
+// out-of-order lgkm event.  The caller counts the DMA itself (vmcnt) and
+// orders LDS accesses around it with "memory" asm.  M0 is written and
+// restored inside the statement (compiler-reserved).
+MDE_DEV void glds16_asm(const void* src, unsigned lds_dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds_dst)
+               : "memory");
+}
+// workgroup barrier without __syncthreads()'s fence (which drains vmcnt, i.e.
+// also the epilogue's global stores): own LDS accesses retired, s_barrier
+MDE_DEV void lds_sync() {
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
 
 typedef f16 f16x2c __attribute__((ext_vector_type(2)));
 
@@ -369,6 +390,314 @@ hipError_t conv_tiles(const GemmParams& p, hipStream_t st) {
     if (!UP && conv_narrow_tiles() && wg128 < 512) return run_conv<64, 4, 1, CK, S, UP, EM>(p, st);
     return run_conv<128, 2, 2, CK, S, UP, EM>(p, st);
   }
+}
+
+// ---------------------------------------------------------------------------
+// Persistent 64 -> 64 channel direct conv (the DPT RCU convs at 64 features,
+// stride 1): conv3_kernel streams the 9 weight taps (72 KB) through LDS once
+// per 128-pixel tile -- 576 B of L2 -> LDS traffic per output pixel beside
+// ~180 B of patch, and a barrier per tap.  Here one workgroup per CU keeps
+// the whole weight set LDS-resident, walks a run of tiles, and prefetches the
+// next tile's patch into the second of two patch buffers while the MFMAs run
+// on the first; the tap loop has no barrier.  Same fragments and MFMA order
+// as conv3_kernel at CK 64 (one chunk, taps in order, two k-steps each):
+// bit-identical.
+// The tap loop is address-free: every fragment read is one of 16 per-lane
+// patch addresses (the chunk swizzle of pixel pp depends on (pp & 7) only,
+// and a tap moves pp by a compile-time amount) or 4 weight addresses, plus an
+// immediate offset -- the tile loop is unrolled by two so the patch buffer
+// is a constant too (computed addresses cost ~3 VALU per MFMA, which the
+// 8 issue cycles an MFMA leaves cannot hold).  The input ReLU (conv1) is one
+// LDS pass over each landed patch, not 4 VALU per fragment read.
+// MODE (the two RCU convs): 0 = ReLU'd input, bias, ReLU, no residual
+// (conv1); 1 = bias + res0; 2 = bias + res0 + res1 (conv2).  Its own
+// epilogue: the residual rows are loaded before the MFMAs and consumed on
+// every path (rows outside the map load row 0 and skip the store), so no load
+// is left pending across the tile loop -- hipcc otherwise guards the next
+// iteration with vmcnt(0), draining the patch prefetch before the first read.
+// The tile parks in the patch buffer just consumed: f16 rows (MODE 0: the f16
+// value is the output) or fp32 in two 16-row passes, then leaves as whole
+// 128-B rows.
+// TYP = 16 (the default, switch value 1): 16 x 16-pixel tiles on 8 waves,
+// LDS 154 KB; 8 (value 2, A/B): 8 x 16 on 4 waves, 118 KB -- one wave per
+// SIMD, measured slower.  Each wave: 2 tile rows x 64 channels.
+template <int TYP, int MODE>
+__global__ void __launch_bounds__(TYP * 32) __attribute__((amdgpu_waves_per_eu(1)))
+conv64p_kernel(const GemmParams p) {
+  constexpr int NW = TYP / 2, NT = NW * 64, TM = 2, TN = 4;
+  constexpr int ROWB = 128, RWP = 8;  // patch / weight rows of 64 halves, rows per wave-instruction
+  constexpr int PH = TYP + 2, PW = TW + 2, PHW = PH * PW;
+  constexpr int PINS = (PHW + RWP - 1) / RWP;
+  constexpr int PATCH = PINS * RWP * ROWB;
+  constexpr int WOFF = 2 * PATCH;  // weights after the two patch buffers: row (tap, n) at WOFF + (tap * 64 + n) * 128
+  constexpr int WB = 9 * 64 * ROWB;
+  constexpr int EPIW = 16 * 64 * 4;  // staging slice per wave: 16 fp32 rows (or 32 f16 rows)
+  constexpr int NRES = MODE;
+  static_assert(NW * EPIW <= PATCH, "epilogue staging fits the consumed patch buffer");
+  static_assert(PATCH + ((TM + 1) * PW + 2) * ROWB < 65536 && 7 * 8192 + 3 * 2048 < 65536, "ds_read immediate offsets");
+  static_assert(PW % 8 == 2, "pixel row stride = 2 mod 8 (the swizzle table below)");
+  __shared__ __attribute__((aligned(16))) char smem[2 * PATCH + WB];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int Ho = p.oh, Wo = p.ow;
+  const int tiles_x = (Wo + TW - 1) / TW, tiles_y = (Ho + TYP - 1) / TYP;
+  const int ntiles = p.cb * tiles_x * tiles_y;
+  // XCD x (= blockIdx % 8, one L2) owns tiles [x nt / 8, (x+1) nt / 8); its
+  // workgroups stride through the run, so the tiles in flight on an XCD are
+  // neighbours sharing halo rows in its L2 (as upconv_kernel)
+  const int x8 = blockIdx.x & 7, g8 = (int)gridDim.x >> 3;
+  int t = (int)((long long)x8 * ntiles / 8) + (int)(blockIdx.x >> 3);
+  const int tend = (int)((long long)(x8 + 1) * ntiles / 8);
+  if (t >= tend) return;  // uniform, before any load
+
+  const int lrow = lane >> 3;
+  const int lch = cpch<64>(lrow, lane & 7);  // logical chunk this lane fetches (glds)
+  const size_t imgsz = (size_t)p.ch * p.cw * 64;
+
+  // ---- the weight set, once
+  for (int q = wave; q < 9 * 64 / RWP; q += NW) {
+    const int tap = q >> 3, n = (q & 7) * RWP + lrow;
+    glds16c(reinterpret_cast<const f16*>(p.W) + (size_t)n * p.ldw + tap * 64 + lch * 8, smem + WOFF + q * RWP * ROWB);
+  }
+  // ASM: the in-loop prefetch (glds16_asm); the prologue's patch uses the
+  // builtin, drained by __syncthreads()'s vmcnt(0) before the loop
+  auto load_patch = [&](int tt, int buf, auto asm_tag) {
+    const int tx = tt % tiles_x, r = tt / tiles_x;
+    const int ty = r % tiles_y, b = r / tiles_y;
+    const int iy0 = ty * TYP - 1, ix0 = tx * TW - 1;
+    const f16* img = reinterpret_cast<const f16*>(p.A) + (size_t)b * imgsz;
+    char* dst = smem + buf * PATCH;
+    for (int q = wave; q < PINS; q += NW) {
+      const int pp = q * RWP + lrow;
+      const int py = pp / PW, px = pp - (pp / PW) * PW;
+      const int iy = iy0 + py, ix = ix0 + px;
+      const bool ok = pp < PHW && iy >= 0 && iy < p.ch && ix >= 0 && ix < p.cw;
+      const f16* src = ok ? img + ((size_t)iy * p.cw + ix) * 64 + lch * 8 : g_zero_conv;
+      if constexpr (decltype(asm_tag)::value)
+        glds16_asm(src, __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(dst + q * RWP * ROWB)));
+      else
+        glds16c(src, dst + q * RWP * ROWB);
+    }
+  };
+  // MODE 0: ReLU of a landed patch, in place (callers barrier before and after)
+  auto relu_patch = [&](int buf) {
+    for (int c = tid; c < PATCH / 16; c += NT) {
+      f16x8* q = reinterpret_cast<f16x8*>(smem + buf * PATCH + c * 16);
+      *q = relu8(*q);
+    }
+  };
+
+  // fragment addresses.  Patch: pixel pp = (wave TM + i + ky) PW + (lane & 15)
+  // + kx, logical chunk lc = 4 s + (lane >> 4) at physical chunk lc ^ (pp & 7);
+  // with PW = 2 mod 8, pp & 7 = (u + e) & 7 for u = (2 wave TM + (lane & 15))
+  // and e = 2 (i + ky) + kx, so the 16 (e & 7, s) addresses below plus the
+  // immediate ((i + ky) PW + kx) * 128 + BUF * PATCH cover every read.
+  // Weights: row j 16 + (lane & 15) of a tap, (row & 7) = (lane & 7).
+  int pa[8][2], wa[2], wa8[2];
+  {
+    const int u = 2 * wave * TM + (lane & 15);
+    const int rowbase = ((wave * TM) * PW + (lane & 15)) * ROWB;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) pa[e][s2] = rowbase + ((((4 * s2 + (lane >> 4)) ^ ((u + e) & 7))) << 4);
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2) {
+      wa[s2] = WOFF + (lane & 15) * ROWB + (((4 * s2 + (lane >> 4)) ^ (lane & 7)) << 4);
+      wa8[s2] = wa[s2] + 8 * 64 * ROWB;
+    }
+  }
+
+  // epilogue geometry: the MFMA layout parks column quad (lane >> 4) of
+  // pixel row (lane & 15); the read-back lane owns row (lane >> 3) of each
+  // 8-row group and channels 8 (lane & 7) .. + 7
+  const int rr = lane >> 3, c8 = lane & 7;
+  float4 bias[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) bias[j] = *reinterpret_cast<const float4*>(p.bias + j * 16 + (lane >> 4) * 4);
+
+  load_patch(t, 0, std::false_type{});
+  wait_vmc();
+  __syncthreads();
+  if constexpr (MODE == 0) {
+    relu_patch(0);
+    lds_sync();
+  }
+
+  // one tile: MFMAs on patch buffer BUF while the next tile's patch lands in
+  // the other; returns true when the workgroup's run is done
+  auto step = [&](auto buf_tag) -> bool {
+    constexpr int BUF = decltype(buf_tag)::value;
+    const int tn = t + g8;
+    // (every wave's epilogue staging in BUF ^ 1 was read before the barrier
+    // that ended the previous tile)
+    if (tn < tend) load_patch(tn, BUF ^ 1, std::true_type{});
+
+    const int tx = t % tiles_x, r = t / tiles_x;
+    const int ty = r % tiles_y, b = r / tiles_y;
+    // output row (pixel) of read-back row it * 8 + rr of this wave, or -1
+    int mo[4];
+#pragma unroll
+    for (int it = 0; it < 4; ++it) {
+      const int row = it * 8 + rr;
+      const int oy = ty * TYP + wave * TM + (row >> 4), ox = tx * TW + (row & 15);
+      mo[it] = (oy < Ho && ox < Wo) ? ((b * Ho + oy) * Wo + ox) : -1;
+    }
+    // residual rows, loaded now and consumed after the MFMAs on every path
+    f16x8 res[NRES > 0 ? NRES : 1][4];
+    if constexpr (NRES > 0) {
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const size_t o = (size_t)(mo[it] < 0 ? 0 : mo[it]) * p.ldo + c8 * 8;
+        res[0][it] = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res0) + o);
+        if constexpr (NRES > 1) res[1][it] = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res1) + o);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);  // issue the loads here, not sunk next to their use behind the MFMAs
+
+    f32x4 acc[TM][TN];
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap) {
+      const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        f16x8 fa[TM], fb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int e = 2 * (i + ky) + kx;
+          fa[i] = *reinterpret_cast<const f16x8*>(smem + pa[e & 7][s2] + (BUF * PATCH + ((i + ky) * PW + kx) * ROWB));
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+          fb[j] = *reinterpret_cast<const f16x8*>(smem + (tap < 8 ? wa[s2] + tap * 64 * ROWB : wa8[s2]) + j * 16 * ROWB);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);  // (tap MFMAs)
+      }
+    }
+    // (the epilogue's residual conversions stay below: hoisted among the
+    // MFMAs they would wait for the loads -- and, in order, the prefetch)
+    __builtin_amdgcn_sched_barrier(0);
+    // the next patch landed (own DMAs; the previous tile's stores and this
+    // tile's residual loads, all issued before the MFMAs, too) -- after the
+    // barrier every wave's DMAs and patch reads are done: the epilogue may
+    // stage in this buffer and the next tile read the other
+    wait_vmc();
+    lds_sync();
+    if constexpr (MODE == 0) {
+      if (tn < tend) relu_patch(BUF ^ 1);
+    }
+
+    char* stage = smem + BUF * PATCH + wave * EPIW;
+    f16* const out = reinterpret_cast<f16*>(p.out16);
+    if constexpr (MODE == 0) {
+      // f16 rows: row r at r * 128, 16-B chunk c swizzled by (r & 7)
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const float4 bn = bias[j];
+          const float v0 = acc[i][j][0] + bn.x, v1 = acc[i][j][1] + bn.y;
+          const float v2 = acc[i][j][2] + bn.z, v3 = acc[i][j][3] + bn.w;
+          const f16x4 h = {(f16)(v0 > 0.f ? v0 : 0.f), (f16)(v1 > 0.f ? v1 : 0.f), (f16)(v2 > 0.f ? v2 : 0.f),
+                           (f16)(v3 > 0.f ? v3 : 0.f)};
+          const int row = i * 16 + (lane & 15), q = j * 4 + (lane >> 4);  // 8-B column quad
+          *reinterpret_cast<f16x4*>(stage + row * 128 + ((((q >> 1) ^ (row & 7)) << 4) | ((q & 1) << 3))) = h;
+        }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int row = it * 8 + rr;
+        const f16x8 h = *reinterpret_cast<const f16x8*>(stage + row * 128 + ((c8 ^ (row & 7)) << 4));
+        if (mo[it] >= 0) *reinterpret_cast<f16x8*>(out + (size_t)mo[it] * p.ldo + c8 * 8) = h;
+      }
+    } else {
+      // fp32 rows of 256 B, 16-B chunk c swizzled by (r & 7); two passes of
+      // 16 rows (accumulator row block i)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        if (i > 0) __builtin_amdgcn_wave_barrier();  // pass 0's reads before pass 1 overwrites the slice
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const float4 bn = bias[j];
+          const f32x4 v = {acc[i][j][0] + bn.x, acc[i][j][1] + bn.y, acc[i][j][2] + bn.z, acc[i][j][3] + bn.w};
+          const int row = lane & 15, q = j * 4 + (lane >> 4);  // 16-B chunk
+          *reinterpret_cast<f32x4*>(stage + row * 256 + ((q ^ (row & 7)) << 4)) = v;
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int h2 = 0; h2 < 2; ++h2) {
+          const int it = i * 2 + h2, row = h2 * 8 + rr;
+          const f32x4 a = *reinterpret_cast<const f32x4*>(stage + row * 256 + (((2 * c8) ^ (row & 7)) << 4));
+          const f32x4 bb = *reinterpret_cast<const f32x4*>(stage + row * 256 + (((2 * c8 + 1) ^ (row & 7)) << 4));
+          float v[8] = {a[0], a[1], a[2], a[3], bb[0], bb[1], bb[2], bb[3]};
+          const f16x8 r0 = res[0][it];
+          if (p.res0_relu) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += fmaxf((float)r0[e], 0.f);
+          } else {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += (float)r0[e];
+          }
+          if constexpr (NRES > 1) {
+            const f16x8 r1 = res[NRES - 1][it];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] += (float)r1[e];
+          }
+          f16x8 h;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) h[e] = (f16)v[e];
+          if (mo[it] >= 0) *reinterpret_cast<f16x8*>(out + (size_t)mo[it] * p.ldo + c8 * 8) = h;
+        }
+      }
+    }
+    if (tn >= tend) return true;
+    lds_sync();  // staging reads retired before the next prefetch overwrites them; the next patch is ReLU'd (stores stay in flight)
+    t = tn;
+    return false;
+  };
+  for (;;) {
+    if (step(std::integral_constant<int, 0>{})) break;
+    if (step(std::integral_constant<int, 1>{})) break;
+  }
+}
+
+// Persistent conv for the RCU shapes (64 -> 64 channels, stride 1, E_STORE
+// with bias: conv1 = ReLU'd input + ReLU, conv2 = residual(s), no
+// activation) on grids of >= 4 tiles per CU (switch "conv_persist"): ViT-S's
+// 148^2 / 74^2 RCUs at batch >= 8
+bool conv64p_launch(const GemmParams& p, hipStream_t st, hipError_t& err) {
+  const int mode = knob(KNOB_CONV_PERSIST);
+  if (!mode || p.amode != A_CONV3 || p.emode != E_STORE || p.stride != 1 || p.N != 64 || p.cc != 64 || !p.bias ||
+      p.ch != p.oh || p.cw != p.ow || p.ldo < 64 || (p.ldo & 7) || p.res0_rows > 0)
+    return false;
+  int m;
+  if (p.relu_in && p.act == ACT_RELU && !p.res0 && !p.res1) m = 0;
+  else if (!p.relu_in && p.act == ACT_NONE && p.res0) m = p.res1 ? 2 : 1;
+  else return false;
+  const int typ = mode == 2 ? 8 : 16;
+  const long long tiles = (long long)p.cb * ((p.oh + typ - 1) / typ) * ((p.ow + TW - 1) / TW);
+  if (tiles < 4 * 256 || tiles >= (1ll << 31)) return false;
+  const dim3 grid(256), block(typ * 32);
+  if (typ == 16) {
+    if (m == 0) hipLaunchKernelGGL((conv64p_kernel<16, 0>), grid, block, 0, st, p);
+    else if (m == 1) hipLaunchKernelGGL((conv64p_kernel<16, 1>), grid, block, 0, st, p);
+    else hipLaunchKernelGGL((conv64p_kernel<16, 2>), grid, block, 0, st, p);
+  } else {
+    if (m == 0) hipLaunchKernelGGL((conv64p_kernel<8, 0>), grid, block, 0, st, p);
+    else if (m == 1) hipLaunchKernelGGL((conv64p_kernel<8, 1>), grid, block, 0, st, p);
+    else hipLaunchKernelGGL((conv64p_kernel<8, 2>), grid, block, 0, st, p);
+  }
+  err = hipGetLastError();
+  return true;
 }
 
 // ---------------------------------------------------------------------------
@@ -747,6 +1076,8 @@ hipError_t launch_conv3(const GemmParams& p, hipStream_t st) {
     return ck64 ? conv_tiles<64, 1, false, E_HEAD>(p, st) : conv_tiles<32, 1, false, E_HEAD>(p, st);
   }
   if (p.emode != E_STORE) return hipErrorInvalidValue;
+  hipError_t err;
+  if (!up && conv64p_launch(p, st, err)) return err;
   if (up) return ck64 ? conv_tiles<64, 1, true, E_STORE>(p, st) : conv_tiles<32, 1, true, E_STORE>(p, st);
   if (p.stride == 2) return conv_tiles<32, 2, false, E_STORE>(p, st);
   return ck64 ? conv_tiles<64, 1, false, E_STORE>(p, st) : conv_tiles<32, 1, false, E_STORE>(p, st);

@@ -34,6 +34,10 @@ enum Knob : int {
   // 8 waves on small-grid 128^2 tiles (1: on).
   // test_gemm_small_grid_variants_bit_exact
   KNOB_W8SMALL,
+  // persistent 64 -> 64 channel direct conv with LDS-resident weights (0 off,
+  // 1: 16 x 16-pixel tiles on 8 waves, 2: 8 x 16 on 4 waves).
+  // test_conv_persist_bit_exact
+  KNOB_CONV_PERSIST,
   KNOB_COUNT
 };
 

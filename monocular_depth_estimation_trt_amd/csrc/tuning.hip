@@ -26,6 +26,7 @@ constexpr KnobDef kKnobs[KNOB_COUNT] = {
     {"gemm256", "MDE_GEMM256", 1, 0, 2},
     {"deep64", "MDE_GEMM_DEEP64", 1, 0, 1},
     {"w8small", "MDE_GEMM_W8SMALL", 1, 0, 1},
+    {"conv_persist", "MDE_CONV_PERSIST", 1, 0, 2},
 };
 
 std::atomic<int> g_val[KNOB_COUNT];

@@ -322,6 +322,40 @@ def test_conv_narrow_tiles_bit_exact(gpu, h, cin, cout):
     assert torch.equal(got[0], got[1]), "narrow conv tiles must equal the wide ones bit for bit"
 
 
+# the persistent 64-channel RCU conv (conv.hip conv64p_kernel): both RCU
+# forms (conv1: ReLU'd input, bias, ReLU; conv2: bias + one or two residuals)
+# on full and ragged tile grids, both tile shapes, bit for bit against the
+# per-tile kernel (conv_persist=0) and against torch
+@pytest.mark.parametrize("B,h,w,relu_in,act,nres", [(12, 148, 148, 1, 1, 0), (12, 148, 148, 0, 0, 1),
+                                                    (12, 148, 148, 0, 0, 2), (14, 150, 133, 1, 1, 0),
+                                                    (14, 150, 133, 0, 0, 2)])
+def test_conv_persist_bit_exact(gpu, B, h, w, relu_in, act, nres):
+    x = rn(B, 64, h, w)
+    wt, b = rn(64, 64, 3, 3, scale=(9 * 64) ** -0.5), rn(64, scale=0.02)
+    xin = x.half().float()
+    ref = F.conv2d(F.relu(xin) if relu_in else xin, wt.half().float(), b, padding=1)
+    if act:
+        ref = F.relu(ref)
+    res = [rn(*ref.shape) for _ in range(nres)]
+    for r in res:
+        ref = ref + r.half().float()
+    wp = conv_w(wt).to(gpu)
+    rg = [nhwc(r).half().to(gpu) for r in res] + [None, None]
+    xg, bg = nhwc(x).half().to(gpu), b.to(gpu)
+    from monocular_depth_estimation_trt_amd import _lib
+    got = []
+    for flag in (0, 1, 2):
+        with _lib.tuning(conv_persist=flag):
+            out = torch.empty(B, h, w, 64, dtype=torch.float16, device=gpu)
+            op("mde_op_conv3x3", ptr(xg), B, h, w, 64, ptr(wp), wp.shape[1], 64, 1, relu_in, ptr(bg), act,
+               ptr(rg[0]), ptr(rg[1]), ptr(out), stream())
+        torch.cuda.synchronize()
+        got.append(out)
+    close(nchw(got[1]), ref, 1e-2, 1e-2, f"persistent conv {B}x{h}x{w} relu_in={relu_in} nres={nres}")
+    assert torch.equal(got[1], got[0]), "persistent conv (8 x 16 tiles) must equal the per-tile kernel bit for bit"
+    assert torch.equal(got[2], got[0]), "persistent conv (16 x 16 tiles) must equal the per-tile kernel bit for bit"
+
+
 # E_STORE split-K (launch_gemm's small-grid policy): the batch-1 ViT-L DPT
 # shapes -- layer4_rn (19^2, 1024 -> 256, im2col), layer3_rn (37^2, direct conv
 # grid), conv_s2 (37^2 -> 19^2, stride 2), an RCU conv with pre-ReLU, bias,

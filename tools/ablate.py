@@ -23,6 +23,16 @@ sys.path.insert(0, ROOT)
 
 # name -> (file, [(old, new, count)])
 VARIANTS = {
+    # persistent RCU conv: no next-patch prefetch (MFMAs re-read the last patch)
+    "cp_nopf": ("conv.hip", [("    if (tn < tend) load_patch(tn, BUF ^ 1, std::true_type{});\n", "", 1)]),
+    # persistent RCU conv: no tap MFMAs (fragments kept live)
+    "cp_nomfma": ("conv.hip", [
+        ("acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);  // (tap MFMAs)",
+         'asm volatile("" :: "v"(fb[j]), "v"(fa[i]));', 1)]),
+    # persistent RCU conv: no output stores (values kept live)
+    "cp_nostore": ("conv.hip", [
+        ("if (mo[it] >= 0) *reinterpret_cast<f16x8*>(out + (size_t)mo[it] * p.ldo + c8 * 8) = h;",
+         'asm volatile("" :: "v"(h));', 2)]),
     # attention: the softmax exponentials replaced by their argument
     "attn_noexp": ("attention.hip", [
         ("const float p0 = __builtin_amdgcn_exp2f(sc[r]), p1 = __builtin_amdgcn_exp2f(sc[r + 1]);",
@@ -93,7 +103,7 @@ VARIANTS = {
     # direct conv (conv3_kernel and upconv_kernel): no MFMAs (fragments kept live)
     "conv_nomfma": ("conv.hip", [
         ("for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);",
-         'for (int j = 0; j < TN; ++j) asm volatile("" :: "v"(fb[j]), "v"(fa[i]));', 3)]),
+         'for (int j = 0; j < TN; ++j) asm volatile("" :: "v"(fb[j]), "v"(fa[i]));', 4)]),
     # separable upsampling conv: pass V without its vertical lerp (one H row read)
     "upconv_nov": ("conv.hip", [
         ("          v = lerp8(a, bb, (f16)ly1);\n", "          v = a;\n          asm volatile(\"\" :: \"v\"(bb));\n", 1)]),
