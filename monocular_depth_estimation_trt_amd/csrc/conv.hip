@@ -410,7 +410,8 @@ hipError_t conv_tiles(const GemmParams& p, hipStream_t st) {
 // 8 issue cycles an MFMA leaves cannot hold).  The input ReLU (conv1) is one
 // LDS pass over each landed patch, not 4 VALU per fragment read.
 // MODE (the two RCU convs): 0 = ReLU'd input, bias, ReLU, no residual
-// (conv1); 1 = bias + res0; 2 = bias + res0 + res1 (conv2).  Its own
+// (conv1); 1 = bias + res0; 2 = bias + res0 + res1 (conv2); 3 = plain (bias
+// optional: layer1_rn, whose 48 input channels are padded to 64).  Its own
 // epilogue: the residual rows are loaded before the MFMAs and consumed on
 // every path (rows outside the map load row 0 and skip the store), so no load
 // is left pending across the tile loop -- hipcc otherwise guards the next
@@ -432,7 +433,8 @@ conv64p_kernel(const GemmParams p) {
   constexpr int WOFF = 2 * PATCH;  // weights after the two patch buffers: row (tap, n) at WOFF + (tap * 64 + n) * 128
   constexpr int WB = 9 * 64 * ROWB;
   constexpr int EPIW = 16 * 64 * 4;  // staging slice per wave: 16 fp32 rows (or 32 f16 rows)
-  constexpr int NRES = MODE;
+  constexpr int NRES = MODE == 3 ? 0 : MODE;
+  constexpr bool F16STAGE = MODE == 0 || MODE == 3;  // no residual: the staged f16 value is the output
   static_assert(NW * EPIW <= PATCH, "epilogue staging fits the consumed patch buffer");
   static_assert(PATCH + ((TM + 1) * PW + 2) * ROWB < 65536 && 7 * 8192 + 3 * 2048 < 65536, "ds_read immediate offsets");
   static_assert(PW % 8 == 2, "pixel row stride = 2 mod 8 (the swizzle table below)");
@@ -515,7 +517,8 @@ conv64p_kernel(const GemmParams p) {
   const int rr = lane >> 3, c8 = lane & 7;
   float4 bias[TN];
 #pragma unroll
-  for (int j = 0; j < TN; ++j) bias[j] = *reinterpret_cast<const float4*>(p.bias + j * 16 + (lane >> 4) * 4);
+  for (int j = 0; j < TN; ++j)
+    bias[j] = p.bias ? *reinterpret_cast<const float4*>(p.bias + j * 16 + (lane >> 4) * 4) : float4{0.f, 0.f, 0.f, 0.f};
 
   load_patch(t, 0, std::false_type{});
   wait_vmc();
@@ -596,7 +599,7 @@ conv64p_kernel(const GemmParams p) {
 
     char* stage = smem + BUF * PATCH + wave * EPIW;
     f16* const out = reinterpret_cast<f16*>(p.out16);
-    if constexpr (MODE == 0) {
+    if constexpr (F16STAGE) {
       // f16 rows: row r at r * 128, 16-B chunk c swizzled by (r & 7)
 #pragma unroll
       for (int i = 0; i < TM; ++i)
@@ -605,8 +608,9 @@ conv64p_kernel(const GemmParams p) {
           const float4 bn = bias[j];
           const float v0 = acc[i][j][0] + bn.x, v1 = acc[i][j][1] + bn.y;
           const float v2 = acc[i][j][2] + bn.z, v3 = acc[i][j][3] + bn.w;
-          const f16x4 h = {(f16)(v0 > 0.f ? v0 : 0.f), (f16)(v1 > 0.f ? v1 : 0.f), (f16)(v2 > 0.f ? v2 : 0.f),
-                           (f16)(v3 > 0.f ? v3 : 0.f)};
+          const f16x4 h = MODE == 0 ? f16x4{(f16)(v0 > 0.f ? v0 : 0.f), (f16)(v1 > 0.f ? v1 : 0.f),
+                                            (f16)(v2 > 0.f ? v2 : 0.f), (f16)(v3 > 0.f ? v3 : 0.f)}
+                                    : f16x4{(f16)v0, (f16)v1, (f16)v2, (f16)v3};
           const int row = i * 16 + (lane & 15), q = j * 4 + (lane >> 4);  // 8-B column quad
           *reinterpret_cast<f16x4*>(stage + row * 128 + ((((q >> 1) ^ (row & 7)) << 4) | ((q & 1) << 3))) = h;
         }
@@ -670,17 +674,18 @@ conv64p_kernel(const GemmParams p) {
   }
 }
 
-// Persistent conv for the RCU shapes (64 -> 64 channels, stride 1, E_STORE
-// with bias: conv1 = ReLU'd input + ReLU, conv2 = residual(s), no
-// activation) on grids of >= 4 tiles per CU (switch "conv_persist"): ViT-S's
+// Persistent conv for the RCU shapes (64 -> 64 channels, stride 1, E_STORE:
+// conv1 = ReLU'd input + bias + ReLU, conv2 = bias + residual(s), and the
+// plain conv of layer1_rn) on grids of >= 4 tiles per CU (switch "conv_persist"): ViT-S's
 // 148^2 / 74^2 RCUs at batch >= 8
 bool conv64p_launch(const GemmParams& p, hipStream_t st, hipError_t& err) {
   const int mode = knob(KNOB_CONV_PERSIST);
-  if (!mode || p.amode != A_CONV3 || p.emode != E_STORE || p.stride != 1 || p.N != 64 || p.cc != 64 || !p.bias ||
+  if (!mode || p.amode != A_CONV3 || p.emode != E_STORE || p.stride != 1 || p.N != 64 || p.cc != 64 ||
       p.ch != p.oh || p.cw != p.ow || p.ldo < 64 || (p.ldo & 7) || p.res0_rows > 0)
     return false;
   int m;
   if (p.relu_in && p.act == ACT_RELU && !p.res0 && !p.res1) m = 0;
+  else if (!p.relu_in && p.act == ACT_NONE && !p.res0 && !p.res1) m = 3;
   else if (!p.relu_in && p.act == ACT_NONE && p.res0) m = p.res1 ? 2 : 1;
   else return false;
   const int typ = mode == 2 ? 8 : 16;
@@ -690,11 +695,13 @@ bool conv64p_launch(const GemmParams& p, hipStream_t st, hipError_t& err) {
   if (typ == 16) {
     if (m == 0) hipLaunchKernelGGL((conv64p_kernel<16, 0>), grid, block, 0, st, p);
     else if (m == 1) hipLaunchKernelGGL((conv64p_kernel<16, 1>), grid, block, 0, st, p);
-    else hipLaunchKernelGGL((conv64p_kernel<16, 2>), grid, block, 0, st, p);
+    else if (m == 2) hipLaunchKernelGGL((conv64p_kernel<16, 2>), grid, block, 0, st, p);
+    else hipLaunchKernelGGL((conv64p_kernel<16, 3>), grid, block, 0, st, p);
   } else {
     if (m == 0) hipLaunchKernelGGL((conv64p_kernel<8, 0>), grid, block, 0, st, p);
     else if (m == 1) hipLaunchKernelGGL((conv64p_kernel<8, 1>), grid, block, 0, st, p);
-    else hipLaunchKernelGGL((conv64p_kernel<8, 2>), grid, block, 0, st, p);
+    else if (m == 2) hipLaunchKernelGGL((conv64p_kernel<8, 2>), grid, block, 0, st, p);
+    else hipLaunchKernelGGL((conv64p_kernel<8, 3>), grid, block, 0, st, p);
   }
   err = hipGetLastError();
   return true;

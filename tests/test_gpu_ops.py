@@ -326,12 +326,15 @@ def test_conv_narrow_tiles_bit_exact(gpu, h, cin, cout):
 # forms (conv1: ReLU'd input, bias, ReLU; conv2: bias + one or two residuals)
 # on full and ragged tile grids, both tile shapes, bit for bit against the
 # per-tile kernel (conv_persist=0) and against torch
-@pytest.mark.parametrize("B,h,w,relu_in,act,nres", [(12, 148, 148, 1, 1, 0), (12, 148, 148, 0, 0, 1),
-                                                    (12, 148, 148, 0, 0, 2), (14, 150, 133, 1, 1, 0),
-                                                    (14, 150, 133, 0, 0, 2)])
-def test_conv_persist_bit_exact(gpu, B, h, w, relu_in, act, nres):
+@pytest.mark.parametrize("B,h,w,relu_in,act,nres,bias", [(12, 148, 148, 1, 1, 0, 1), (12, 148, 148, 0, 0, 1, 1),
+                                                         (12, 148, 148, 0, 0, 2, 1), (14, 150, 133, 1, 1, 0, 1),
+                                                         (14, 150, 133, 0, 0, 2, 1), (12, 148, 148, 0, 0, 0, 0),
+                                                         (14, 150, 133, 0, 0, 0, 1)])
+def test_conv_persist_bit_exact(gpu, B, h, w, relu_in, act, nres, bias):
     x = rn(B, 64, h, w)
     wt, b = rn(64, 64, 3, 3, scale=(9 * 64) ** -0.5), rn(64, scale=0.02)
+    if not bias:
+        b = torch.zeros(64)
     xin = x.half().float()
     ref = F.conv2d(F.relu(xin) if relu_in else xin, wt.half().float(), b, padding=1)
     if act:
@@ -347,8 +350,8 @@ def test_conv_persist_bit_exact(gpu, B, h, w, relu_in, act, nres):
     for flag in (0, 1, 2):
         with _lib.tuning(conv_persist=flag):
             out = torch.empty(B, h, w, 64, dtype=torch.float16, device=gpu)
-            op("mde_op_conv3x3", ptr(xg), B, h, w, 64, ptr(wp), wp.shape[1], 64, 1, relu_in, ptr(bg), act,
-               ptr(rg[0]), ptr(rg[1]), ptr(out), stream())
+            op("mde_op_conv3x3", ptr(xg), B, h, w, 64, ptr(wp), wp.shape[1], 64, 1, relu_in, ptr(bg) if bias else None,
+               act, ptr(rg[0]), ptr(rg[1]), ptr(out), stream())
         torch.cuda.synchronize()
         got.append(out)
     close(nchw(got[1]), ref, 1e-2, 1e-2, f"persistent conv {B}x{h}x{w} relu_in={relu_in} nres={nres}")
