@@ -31,6 +31,9 @@
 // output_conv1 0.259 -> 0.221 ms
 #define MDE_UP_BLEND_F16 1
 #endif
+#ifndef MDE_CONVP_RELU_PASS
+#define MDE_CONVP_RELU_PASS 1  // persistent conv1: input ReLU as an LDS pass per patch (0: on each fragment read)
+#endif
 #ifndef MDE_CONV_BRES
 #define MDE_CONV_BRES 1  // 32-wide convs with one channel chunk: all 9 weight taps LDS-resident (1: CK 32, 2: + CK 64)
 #endif
@@ -524,7 +527,7 @@ conv64p_kernel(const GemmParams p) {
   wait_vmc();
   __syncthreads();
   if constexpr (MODE == 0) {
-    relu_patch(0);
+    if (MDE_CONVP_RELU_PASS) relu_patch(0);
     lds_sync();
   }
 
@@ -574,6 +577,7 @@ conv64p_kernel(const GemmParams p) {
         for (int i = 0; i < TM; ++i) {
           const int e = 2 * (i + ky) + kx;
           fa[i] = *reinterpret_cast<const f16x8*>(smem + pa[e & 7][s2] + (BUF * PATCH + ((i + ky) * PW + kx) * ROWB));
+          if constexpr (MODE == 0 && !MDE_CONVP_RELU_PASS) fa[i] = relu8(fa[i]);
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j)
@@ -594,7 +598,7 @@ conv64p_kernel(const GemmParams p) {
     wait_vmc();
     lds_sync();
     if constexpr (MODE == 0) {
-      if (tn < tend) relu_patch(BUF ^ 1);
+      if (MDE_CONVP_RELU_PASS && tn < tend) relu_patch(BUF ^ 1);
     }
 
     char* stage = smem + BUF * PATCH + wave * EPIW;
