@@ -35,7 +35,12 @@
 #define MDE_CONVP_RELU_PASS 1  // persistent conv1: input ReLU as an LDS pass per patch (0: on each fragment read)
 #endif
 #ifndef MDE_CONV_BRES
-#define MDE_CONV_BRES 1  // 32-wide convs with one channel chunk: all 9 weight taps LDS-resident (1: CK 32, 2: + CK 64)
+// 32-wide convs with one channel chunk: all 9 weight taps LDS-resident (1: CK
+// 32, 2: + CK 64 -- the batch-1 ViT-S RCUs on 32-channel tiles: 36 KB of taps,
+// two workgroups per CU on a 380-workgroup grid; rcu.conv 0.144 -> 0.117 ms,
+// forward 0.825 -> 0.798 ms, b1 1044-1049 -> 1077-1079 FPS, two same-box
+// pairs, gpurun_out/r4s51)
+#define MDE_CONV_BRES 2
 #endif
 
 namespace mde {

@@ -29,6 +29,8 @@ VARIANTS = {
     "cp_nomfma": ("conv.hip", [
         ("acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);  // (tap MFMAs)",
          'asm volatile("" :: "v"(fb[j]), "v"(fa[i]));', 1)]),
+    # direct conv: 32-wide tiles with one 64-channel chunk stream their taps (round-4 default: resident)
+    "conv_bres32": ("conv.hip", [("#define MDE_CONV_BRES 2", "#define MDE_CONV_BRES 1", 1)]),
     # persistent RCU conv: conv1's input ReLU on the fragment reads, no LDS pass
     "cp_relufrag": ("conv.hip", [("#define MDE_CONVP_RELU_PASS 1", "#define MDE_CONVP_RELU_PASS 0", 1)]),
     # persistent RCU conv: no output stores (values kept live)
