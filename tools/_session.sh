@@ -1,6 +1,4 @@
 set -o pipefail
-O=gpurun_out/r4s20
+O=gpurun_out/r4e5
 mkdir -p $O
-timeout -k 10 300 python -u tools/_det.py > $O/det.log 2>&1 || exit 1
-timeout -k 10 120 ./build/mlp_probe > $O/probe.log 2>&1 || exit 1
-bash tools/gpu_tasks.sh $O bench:fused:--no-cpu-baseline,--no-b1
+bash tools/gpu_tasks.sh $O tests smoke bench:def: bench:b1:--batch,1,--no-cpu-baseline bench:vitl1:--encoder,vitl,--batch,1,--no-cpu-baseline
