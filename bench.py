@@ -86,6 +86,18 @@ def log(*a):
     print("[bench]", *a, file=sys.stderr, flush=True)
 
 
+def parse_size(v: str):
+    """'518' -> (518, 518); '392x518' -> (392, 518) (the reference's HxW,
+    tools/size_sweep.py / reports/tune/size_depth_anything_v2.json)."""
+    h, _, w = str(v).lower().partition("x")
+    return int(h), int(w or h)
+
+
+# the reference's published DA-V2 ViT-S size sweep (RTX 3080, TRT fp16, batch 1,
+# mean ms per image incl. copies): reports/tune/size_depth_anything_v2.json
+REF_SIZE_MS = {(392, 518): 3.7605, (518, 518): 4.2852, (672, 896): 10.4632}
+
+
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
@@ -100,12 +112,17 @@ def parse(argv=None):
     p.add_argument("--encoder", default="vits", choices=["vits", "vitb", "vitl"])
     p.add_argument("--precision", default="fp16", choices=["fp16", "fp32"],
                    help="DA-V2 engine precision (get_engine's; fp32 = the exact-fp32 encoder)")
-    p.add_argument("--size", type=int, default=518)
+    p.add_argument("--size", type=parse_size, default=(518, 518),
+                   help="DA-V2 input H or HxW (the reference's size sweep: 392x518, 518x518, 672x896)")
     p.add_argument("--b1-iters", type=int, default=100)
     p.add_argument("--b1-warmup", type=int, default=20)
     p.add_argument("--cpu-seconds", type=float, default=12.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-b1", action="store_true")
+    p.add_argument("--no-pcie", action="store_true", help="skip the PCIe-inclusive streamed-batch leg (value_pcie)")
+    p.add_argument("--oversubscribe", action="store_true",
+                   help="allow more ranks than visible GPUs (a launcher rehearsal: ranks share devices round-robin; "
+                        "the line is marked devices_shared and its scaling field is not a scaling measurement)")
     p.add_argument("--profile-iters", type=int, default=3)
     p.add_argument("--layers-json", default="", help="write the per-layer profile here (rank 0)")
     return p.parse_args(argv)
@@ -132,7 +149,9 @@ def profile_layers(ctx, stream, iters):
 
 
 def traffic_path(model, encoder, B, size, frames=1):
-    tag = f"{model}_{encoder}_b{B}_{size}" + (f"_s{frames}" if model == "vggt" else "")
+    h, w = size if isinstance(size, tuple) else (size, size)
+    st = f"{h}" if h == w else f"{h}x{w}"
+    tag = f"{model}_{encoder}_b{B}_{st}" + (f"_s{frames}" if model == "vggt" else "")
     return os.path.join(ROOT, "profiles", f"traffic_{tag}.json")
 
 
@@ -152,6 +171,7 @@ def pmc_traffic(layer_names, path):
 
 
 def roofline(cfg, B, size, layer_ms, frames=1, traffic_file=""):
+    h, w = size if isinstance(size, tuple) else (size, size)
     fam = cfg.get("family")
     if fam == "depth_pro":
         from monocular_depth_estimation_trt_amd import flops_depth_pro as flops
@@ -161,7 +181,7 @@ def roofline(cfg, B, size, layer_ms, frames=1, traffic_file=""):
         lf = flops.layer_flops(cfg, B, frames)
     else:
         from monocular_depth_estimation_trt_amd import flops
-        lf = flops.layer_flops(cfg, size, size, B)
+        lf = flops.layer_flops(cfg, h, w, B)
     cls_ms, cls_fl, cls_n = {}, {}, {}
     for name, ms in layer_ms.items():
         c = flops.layer_class(name)
@@ -250,6 +270,61 @@ def b1_reference_method(blob, dev, images, warmup, iters, ref_fps, prefix="b1_")
     return {prefix + k: v for k, v in res.items()}
 
 
+def pcie_streamed_region(wl, ctx, steps, warmup, sync, barrier):
+    """The served-batch-stream rate with the copies in (the reference's FPS
+    is wall clock over H2D + compute + D2H, core/bench.py:182-210): each step
+    copies a batch of B images from pinned host memory, runs the forward and
+    copies the depth maps back, double-buffered on three streams -- the H2D of
+    batch i+1 and the D2H of batch i-1 run under the forward of batch i.
+    Returns (seconds for `steps` steps, bytes in per step, bytes out per step)."""
+    import torch
+    host_in = torch.from_numpy(wl.images(wl.B, 0)).pin_memory()
+    host_out = [{k: torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for k, t in wl.y.items()} for _ in range(2)]
+    dev_in = [wl.x, torch.empty_like(wl.x)]
+    dev_out = [wl.y, {k: torch.empty_like(t) for k, t in wl.y.items()}]
+    s_h2d, s_fwd, s_d2h = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    in_ready = [torch.cuda.Event() for _ in range(2)]
+    fwd_done = [torch.cuda.Event() for _ in range(2)]
+    out_free = [torch.cuda.Event() for _ in range(2)]
+
+    def step(i):
+        j = i & 1
+        with torch.cuda.stream(s_h2d):
+            s_h2d.wait_event(fwd_done[j])          # forward i-2 has read dev_in[j]
+            dev_in[j].copy_(host_in, non_blocking=True)
+            in_ready[j].record(s_h2d)
+        s_fwd.wait_event(in_ready[j])
+        s_fwd.wait_event(out_free[j])              # D2H i-2 has read dev_out[j]
+        ctx.set_tensor_address(wl.input_name, dev_in[j].data_ptr())
+        for k, t in dev_out[j].items():
+            ctx.set_tensor_address(k, t.data_ptr())
+        ctx.execute_async_v3(s_fwd.cuda_stream)
+        fwd_done[j].record(s_fwd)
+        with torch.cuda.stream(s_d2h):
+            s_d2h.wait_event(fwd_done[j])
+            for k, t in dev_out[j].items():
+                host_out[j][k].copy_(t, non_blocking=True)
+            out_free[j].record(s_d2h)
+
+    for i in range(max(2, warmup)):               # both slots' graphs captured
+        step(i)
+    sync()
+    if barrier is not None:
+        barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        step(i)
+    sync()
+    el = time.perf_counter() - t0
+    # the context goes back to the resident buffers of the main timed region
+    ctx.set_tensor_address(wl.input_name, wl.x.data_ptr())
+    for k, t in wl.y.items():
+        ctx.set_tensor_address(k, t.data_ptr())
+    bytes_in = host_in.numel() * host_in.element_size()
+    bytes_out = sum(t.numel() * t.element_size() for t in wl.y.values())
+    return el, bytes_in, bytes_out
+
+
 def _timed_cpu(fn, seconds, warmup=True, max_n=200):
     if warmup:
         fn()
@@ -264,6 +339,8 @@ def _timed_cpu(fn, seconds, warmup=True, max_n=200):
 
 def cpu_baseline(cfg, size, seconds):
     import torch
+    h, w = size if isinstance(size, tuple) else (size, size)
+    size = h
     torch.set_num_threads(int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1)))
     if cfg.get("family") == "depth_pro":
         # one full fp32 forward is ~19 TFLOP: the sample is ONE forward, no warmup
@@ -284,10 +361,10 @@ def cpu_baseline(cfg, size, seconds):
     else:
         from oracle import dav2_ref
         from monocular_depth_estimation_trt_amd import weights
-        w = dav2_ref.to_torch(weights.synthetic_state_dict(cfg, 1234))
-        x = torch.from_numpy(weights.synthetic_images(1, size, size, first_seed=0))
-        n, el = _timed_cpu(lambda: dav2_ref.forward(w, cfg, x), seconds)
-        what = (f"{n} x DA-V2 {cfg['encoder']} {size}x{size} batch-1 fp32 forwards of oracle/dav2_ref.py "
+        wt = dav2_ref.to_torch(weights.synthetic_state_dict(cfg, 1234))
+        x = torch.from_numpy(weights.synthetic_images(1, h, w, first_seed=0))
+        n, el = _timed_cpu(lambda: dav2_ref.forward(wt, cfg, x), seconds)
+        what = (f"{n} x DA-V2 {cfg['encoder']} {h}x{w} batch-1 fp32 forwards of oracle/dav2_ref.py "
                 f"(torch CPU) after 1 warmup")
     return {"value": round(n / el, 3), "unit": "images/s", "cores": torch.get_num_threads(), "kind": "port",
             "sample": f"{what}, {el:.1f} s"}
@@ -301,6 +378,7 @@ class Workload:
         synthetic item seeds from `first` on."""
         import torch
         self.frames = 1
+        self.ref_size_ms = None
         self.precision = "fp16"
         self.input_name = "input"
         if a.model == "depth_pro":
@@ -309,6 +387,7 @@ class Workload:
             from monocular_depth_estimation_trt_amd.flops_depth_pro import total_flops
             self.cfg = WD.depth_pro_config("dinov2l16_384")
             self.S = S = self.cfg["img"]
+            self.H = self.W = S
             self.B = B
             self.sd = WD.synthetic_state_dict(self.cfg, 4321)
             self.blob = PD.pack_bytes(self.sd, self.cfg)
@@ -327,6 +406,7 @@ class Workload:
             from monocular_depth_estimation_trt_amd.flops_vggt import total_flops
             self.cfg = WV.vggt_config("vggt_1b")
             self.S = S = self.cfg["img"]
+            self.H = self.W = S
             self.B = B
             self.frames = Fr = a.frames
             self.input_name = "images"
@@ -344,18 +424,23 @@ class Workload:
         else:
             from monocular_depth_estimation_trt_amd import pack, weights
             from monocular_depth_estimation_trt_amd.flops import total_flops
-            self.S = S = a.size
+            self.H, self.W = H, W = a.size
+            self.S = S = (H, W) if H != W else H
             self.B = B
             self.cfg = weights.model_config(a.encoder, "metric")
             self.sd = weights.synthetic_state_dict(self.cfg, 1234)
             self.precision = a.precision
-            self.blob = pack.pack_bytes(self.sd, self.cfg, S, S, precision=a.precision)
-            self.images = lambda n, seed: weights.synthetic_images(n, S, S, first_seed=seed)  # noqa: E731
-            self.outs = {"output": (B, S, S)}
-            self.gflop = total_flops(self.cfg, S, S) / 1e9
+            self.blob = pack.pack_bytes(self.sd, self.cfg, H, W, precision=a.precision)
+            self.images = lambda n, seed: weights.synthetic_images(n, H, W, first_seed=seed)  # noqa: E731
+            self.outs = {"output": (B, H, W)}
+            self.gflop = total_flops(self.cfg, H, W) / 1e9
             self.ref_fps = REF_B1_FPS if a.precision == "fp16" else REF_B1_FP32_FPS
+            if (H, W) != (518, 518) and a.encoder == "vits" and a.precision == "fp16" and (H, W) in REF_SIZE_MS:
+                # the reference's size sweep is the published number at this size
+                self.ref_fps = 1000.0 / REF_SIZE_MS[(H, W)]
+                self.ref_size_ms = REF_SIZE_MS[(H, W)]
             self.label = f"DA-V2 {ENC_LABEL.get(a.encoder, a.encoder)}"
-            self.workload = (f"Depth Anything V2 {a.encoder} {S}x{S} metric head, forward, {a.per_gpu_desc}, "
+            self.workload = (f"Depth Anything V2 {a.encoder} {H}x{W} metric head, forward, {a.per_gpu_desc}, "
                              f"inputs resident in HBM, hipGraph replay")
             self.weights = "synthetic seeded (seed 1234), fan-in scaled"
             self.encoder = a.encoder
@@ -365,12 +450,12 @@ class Workload:
 
     def b1_legs(self, a, dev):
         res = b1_reference_method(self.blob, dev, self.images(1, 0), a.b1_warmup, a.b1_iters, self.ref_fps)
-        if a.model == "depth_anything_v2" and self.precision == "fp16":
+        if a.model == "depth_anything_v2" and self.precision == "fp16" and (self.H, self.W) == (518, 518):
             # (the reference's uint8 A/B is an fp16 engine: reports/uint8_ab/depth_anything_v2.json)
             from monocular_depth_estimation_trt_amd import pack, weights
-            blob_u8 = pack.pack_bytes(self.sd, self.cfg, self.S, self.S, input_format="uint8_nhwc",
+            blob_u8 = pack.pack_bytes(self.sd, self.cfg, self.H, self.W, input_format="uint8_nhwc",
                                       precision=self.precision)
-            res.update(b1_reference_method(blob_u8, dev, weights.synthetic_images_u8(1, self.S, self.S, first_seed=0),
+            res.update(b1_reference_method(blob_u8, dev, weights.synthetic_images_u8(1, self.H, self.W, first_seed=0),
                                            a.b1_warmup, a.b1_iters, REF_B1_U8_FPS, prefix="b1_u8_"))
         return res
 
@@ -417,9 +502,15 @@ def main():
         import torch.distributed as dist
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("gloo", rank=rank, world_size=world)
-    # one rank per GPU; more ranks than visible GPUs (a rehearsal on a smaller
-    # box) share them round-robin -- device_count() does not initialise HIP
-    local = local % max(1, torch.cuda.device_count())
+    # one rank per GPU; more ranks than visible GPUs only as an explicit
+    # launcher rehearsal (--oversubscribe: ranks share devices round-robin) --
+    # device_count() does not initialise HIP
+    ndev = max(1, torch.cuda.device_count())
+    shared = world > ndev
+    if shared and not a.oversubscribe:
+        raise SystemExit(f"{world} ranks but {ndev} visible GPU(s): one rank per GPU "
+                         f"(--oversubscribe for a launcher rehearsal that shares devices)")
+    local = local % ndev
     torch.cuda.set_device(local)
 
     from monocular_depth_estimation_trt_amd import replicas
@@ -448,6 +539,21 @@ def main():
                                dist.barrier if dist is not None else None)
     per_rank = replicas.gather_to_rank0(round(el, 6))
     el = replicas.max_over_ranks(el)
+    pcie = None
+    if not a.no_pcie:
+        if ctx is not None:
+            el_p, b_in, b_out = pcie_streamed_region(wl, ctx, a.steps, a.warmup, torch.cuda.synchronize,
+                                                     dist.barrier if dist is not None else None)
+        else:  # an idle rank of a strong-scaling run still joins the barrier
+            if dist is not None:
+                dist.barrier()
+            el_p, b_in, b_out = 0.0, 0, 0
+        el_p = replicas.max_over_ranks(el_p)
+        pcie = {"value_pcie": round(total_items * wl.frames * a.steps / el_p, 2), "ms_per_step_pcie": round(el_p / a.steps * 1e3, 4),
+                "pcie_h2d_mb_per_step": round(b_in / 1e6, 1), "pcie_d2h_mb_per_step": round(b_out / 1e6, 1),
+                "pcie_method": "pinned host batch -> H2D stream -> forward (graph) -> D2H stream into pinned host, "
+                               "double-buffered device I/O, H2D(i+1) and D2H(i-1) under forward(i); wall clock "
+                               "over K steps bracketed by barrier + device sync, max over ranks"}
     out_ok = all(bool(torch.isfinite(t).all().item()) for t in wl.y.values()) if B > 0 else True
     value = total_items * wl.frames * a.steps / el
     ms_step = el / a.steps * 1e3
@@ -487,9 +593,14 @@ def main():
         cpu = cpu_baseline(wl.cfg, S, a.cpu_seconds)
     for c, v in list(breakdown.items())[:10]:
         log(f"{c:24s} {v['ms']:9.4f} ms  x{v['launches']:3d}  {v['tflops']} TF/s")
-    config = {"workload": wl.workload, "encoder": wl.encoder, "img": [S, S], "batch_per_gpu": B,
+    config = {"workload": wl.workload, "encoder": wl.encoder, "img": [wl.H, wl.W], "batch_per_gpu": B,
               "global_batch": total_items, "parallelism": f"replica x{world} (batch shards, no collectives)",
-              "weights": wl.weights}
+              "weights": wl.weights, "physical_gpus": min(world, ndev)}
+    if shared:
+        # a rehearsal of the launch path: the ranks shared devices, so neither
+        # n_gpus nor the value says anything about multi-GPU scaling
+        config["devices_shared"] = True
+        scaling = "none (rehearsal: devices shared)"
     if a.model == "vggt":
         config["frames"] = wl.frames
         # oracle/vggt_ref.py: the aggregator (q/k norm, 2-D RoPE, frame/global
@@ -497,7 +608,7 @@ def main():
         # the reference to pin it
         config["parity"] = "partially pinned: aggregator parity unpinned"
     line = {
-        "metric": f"depth FPS (images/s) at {S}x{S} {wl.precision}, {wl.label}, MI355X",
+        "metric": f"depth FPS (images/s) at {wl.H}x{wl.W} {wl.precision}, {wl.label}, MI355X",
         "value": round(value, 2), "unit": "images/s", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
         "ms_per_step": round(ms_step, 4), "higher_is_better": True, "scaling": scaling,
         "vs_baseline": None, "throughput_vs_ref_b1": round(value / wl.ref_fps, 3),
@@ -510,7 +621,13 @@ def main():
         "cpu_baseline": cpu,
         "output_finite": out_ok,
     }
+    if pcie:
+        line.update(pcie)
     line.update(res_b1)
+    if wl.ref_size_ms:
+        line["b1_ref_ms"] = wl.ref_size_ms
+        line["b1_ref_source"] = ("reports/tune/size_depth_anything_v2.json (RTX 3080 TRT fp16, batch 1, "
+                                 f"{wl.H}x{wl.W})")
     print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()

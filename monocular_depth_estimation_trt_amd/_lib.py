@@ -14,7 +14,18 @@ import os
 import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("MDE_LIB", os.path.join(HERE, "libmde_hip.so"))
+LIB_PATH = os.path.join(HERE, "libmde_hip.so")
+
+
+def use_library(path: str) -> None:
+    """Load a tuning-variant build (tools/ablate.py, tools/bench_kernels.py
+    --lib) instead of the in-tree product library.  Must run before the first
+    lib() call; the product path never calls it (no environment read here:
+    the library's dispatch switches, mde.h mde_tuning_*, are the only knobs)."""
+    global LIB_PATH
+    if _lib is not None and os.path.abspath(path) != os.path.abspath(LIB_PATH):
+        raise RuntimeError(f"libmde_hip already loaded from {LIB_PATH}")
+    LIB_PATH = path
 
 c_void_p, c_int, c_float, c_size_t, c_char_p = C.c_void_p, C.c_int, C.c_float, C.c_size_t, C.c_char_p
 c_int64 = C.c_int64

@@ -77,8 +77,9 @@ __global__ void __launch_bounds__(256) gemm32_kernel(const Gemm32Params p) {
   auto issue = [&](int kt, int buf) {
     char* sb = smem + buf * STAGE;
     const int k0 = kt * 32;
-    // K tail: W is zero-padded to ldw, A is read at a clamped column (any finite value)
-    const int ka = k0 + lch * 4 < p.K ? k0 : 0;
+    // K tail: W is zero-padded to ldw; a lane whose chunk lies past K reads
+    // column 0 of its row instead (finite, and inside the row even when K < 32)
+    const int ka = k0 + lch * 4 < p.K ? k0 : -lch * 4;
 #pragma unroll
     for (int i = 0; i < APASS; ++i) glds16f(arow[i] + ka, sb + (wave + i * NW) * RW * ROWB);
 #pragma unroll

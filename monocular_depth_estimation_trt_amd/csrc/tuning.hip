@@ -1,5 +1,6 @@
 // The dispatch-switch table of libmde_hip (tuning.h) and its C ABI.
 #include <atomic>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <mutex>
@@ -24,8 +25,8 @@ constexpr KnobDef kKnobs[KNOB_COUNT] = {
     {"conv_narrow", "MDE_CONV_NARROW", 1, 0, 1},
     {"upconv", "MDE_UPCONV", 1, 0, 1},
     {"gemm256", "MDE_GEMM256", 1, 0, 2},
-    {"deep64", "MDE_GEMM_DEEP64", 1, 0, 1},
-    {"w8small", "MDE_GEMM_W8SMALL", 1, 0, 1},
+    {"deep64", "MDE_DEEP64", 1, 0, 1},
+    {"w8small", "MDE_W8SMALL", 1, 0, 1},
     {"conv_persist", "MDE_CONV_PERSIST", 1, 0, 2},
 };
 
@@ -39,7 +40,11 @@ void init_once() {
       if (const char* e = std::getenv(kKnobs[i].env)) {  // the library's only environment read
         char* end = nullptr;
         const long x = std::strtol(e, &end, 10);
-        if (end != e && x >= kKnobs[i].lo && x <= kKnobs[i].hi) v = (int)x;
+        if (end != e && *end == '\0' && x >= kKnobs[i].lo && x <= kKnobs[i].hi)
+          v = (int)x;
+        else  // a rejected value is reported, never silently dropped
+          std::fprintf(stderr, "[mde] %s=%s ignored (accepted: integer %d..%d); using %d\n", kKnobs[i].env, e,
+                       kKnobs[i].lo, kKnobs[i].hi, v);
       }
       g_val[i].store(v, std::memory_order_relaxed);
     }

@@ -71,12 +71,17 @@ class Engine:
         self._h = C.c_void_p(handle)
         self.device = device
         self.path = path
+        self._contexts = weakref.WeakSet()
         # torch imported after libmde_hip was loaded maps a second HIP runtime
-        # (_lib.check_single_runtime): refuse to run in that state
-        _lib.check_single_runtime()
+        # (_lib.check_single_runtime): refuse to run in that state -- and free
+        # the packed weights the handle already holds on the device
+        try:
+            _lib.check_single_runtime()
+        except Exception:
+            self.destroy()
+            raise
         self._profile = tuple(tuple(int(v) for v in s) for s in profile) if profile else None
         self._static_batch = int(static_batch)
-        self._contexts = weakref.WeakSet()
         info = _lib.mde_engine_info()
         call("mde_engine_get_info", self._h, C.byref(info))
         self.info = info

@@ -103,9 +103,11 @@ def _run_py(code, env=None):
 def test_tuning_reads_environment_once(lib_path):
     rc, out = _run_py("from monocular_depth_estimation_trt_amd import _lib\n"
                       "print(_lib.get_tuning('splitk'), _lib.get_tuning('gemm256'), _lib.get_tuning('w8small'))",
-                      {"MDE_SPLITK": "0", "MDE_GEMM256": "2", "MDE_GEMM_W8SMALL": "bogus"})
+                      {"MDE_SPLITK": "0", "MDE_GEMM256": "2", "MDE_W8SMALL": "bogus"})
     assert rc == 0, out
-    assert out.split()[-3:] == ["0", "2", "1"], out
+    vals = [l for l in out.splitlines() if not l.startswith("[mde]")][-1]
+    assert vals.split() == ["0", "2", "1"], out
+    assert "MDE_W8SMALL=bogus ignored" in out, out
 
 
 def test_one_hip_runtime_when_torch_comes_first(lib_path):

@@ -638,6 +638,22 @@ def test_linear32(gpu, m, n, k, act):
     close(out, ref.float(), 2e-5, 2e-5, f"linear32 {m}x{n}x{k} act{act}")
 
 
+def test_linear32_k_below_one_step(gpu):
+    """K = 16 < one 32-deep K-step, A rows padded to lda = 32 with NaN: the
+    tail lanes must not read columns >= K (NaN * 0 = NaN)."""
+    m, n, k, lda = 77, 96, 16, 32
+    a, w, b = rn(m, k), rn(n, k, scale=k ** -0.5), rn(n, scale=0.1)
+    ap = torch.full((m, lda), float("nan"))
+    ap[:, :k] = a
+    ref = F.relu(a.double() @ w.double().T + b.double())
+    wp = pad_w32(w).to(gpu)
+    out = torch.empty(m, n, device=gpu)
+    op("mde_op_linear32", ptr(ap.to(gpu)), lda, ptr(wp), wp.shape[1], m, n, k, ptr(b.to(gpu)), 1, ptr(out), n,
+       stream())
+    assert torch.isfinite(out).all()
+    close(out, ref.float(), 2e-5, 2e-5, "linear32 K=16")
+
+
 def test_linear_residual32(gpu):
     m, n, k = 1370, 384, 1536
     a, w, b = rn(m, k), rn(n, k, scale=k ** -0.5), rn(n, scale=0.1)

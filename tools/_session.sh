@@ -1,4 +1,4 @@
 set -o pipefail
-O=gpurun_out/r4e5
+O=gpurun_out/r5s1
 mkdir -p $O
-bash tools/gpu_tasks.sh $O tests smoke bench:def: bench:b1:--batch,1,--no-cpu-baseline bench:vitl1:--encoder,vitl,--batch,1,--no-cpu-baseline
+bash tools/gpu_tasks.sh $O probe:p:4000,20 kpmc:attn48:--batch,48,--only,attention bench:def: bench:vitl1:--encoder,vitl,--batch,1,--no-cpu-baseline

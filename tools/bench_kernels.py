@@ -28,11 +28,11 @@ def main():
     ap.add_argument("--cold", action="store_true",
                     help="also time each launch alone after a 512 MB write (caches cold, as in the graph)")
     a = ap.parse_args()
-    if a.lib:
-        os.environ["MDE_LIB"] = a.lib
     import torch
     from gpu_util import conv_w, pad_w, ptr, stream
     from monocular_depth_estimation_trt_amd import _lib
+    if a.lib:
+        _lib.use_library(a.lib)
     dev = torch.device("cuda:0")
     B, T, D, H = a.batch, a.tokens, a.dim, a.heads
     M = B * T

@@ -8,6 +8,7 @@
 #   tests[:EXPR]          pytest -m gpu (optionally -k EXPR)          -> OUT/tests.log
 #   smoke                 __graft_entry__ smoke()                     -> OUT/smoke.log
 #   peak                  tools/mfma_peak.hip (f16 MFMA peak)         -> OUT/mfma_peak.json
+#   probe[:ITERS,LAUNCHES] tools/dma_war_probe.hip (LDS-DMA address WAR) -> OUT/dma_war_probe.json
 #   bench:TAG:ARGS        python bench.py ARGS (ARGS comma-separated) -> OUT/bench_TAG.json/.err
 #   profile:TAG:ARGS      tools/profile_round.sh (stats + FETCH/WRITE passes) -> OUT/prof_TAG/
 #   pmc:TAG:ARGS          tools/pmc_profile.sh on bench.py ARGS (SQ/TCC passes) -> OUT/pmc_TAG/
@@ -36,6 +37,10 @@ for t in "$@"; do
     peak)
       [ -x build/mfma_peak ] || hipcc -O3 --offload-arch=gfx950 -o build/mfma_peak tools/mfma_peak.hip || exit 1
       timeout -k 10 120 ./build/mfma_peak > "$O/mfma_peak.json" 2> "$O/mfma_peak.err" || { log "peak rc=$?"; exit 1; } ;;
+    probe)
+      [ -x build/dma_war_probe ] || hipcc -O3 --offload-arch=gfx950 -o build/dma_war_probe tools/dma_war_probe.hip || exit 1
+      timeout -k 10 180 ./build/dma_war_probe "${args[@]}" > "$O/dma_war_probe.json" 2> "$O/dma_war_probe.err" \
+        || { log "probe rc=$?"; exit 1; } ;;
     bench)
       timeout -k 10 600 python -u bench.py "${args[@]}" > "$O/bench_$tag.json" 2> "$O/bench_$tag.err" \
         || { log "bench rc=$?"; tail -20 "$O/bench_$tag.err"; exit 1; } ;;
