@@ -39,3 +39,45 @@ def test_product_lds_dma_uses_the_64bit_address_form():
         assert not re.findall(r"global_load_lds_dword\w*\s+v\d+, s\[", txt), src
         assert not re.findall(r"buffer_load_\w+[^\n]*\blds\b", txt), src
     assert seen > 0
+
+
+@pytest.mark.skipif(not os.path.exists(OBJDUMP), reason="ROCm llvm-objdump absent")
+def test_product_has_no_unclear_dma_address_reuse():
+    """tools/dma_hazard_scan.py over the product objects: no ds_read takes
+    the address registers of an in-flight LDS-DMA of a form the probe did not
+    clear (only the 64-bit vaddr form is in the library, and its reuse sites
+    are cleared by tools/dma_war_probe.hip, profiles/r05_dma_war_probe.json;
+    the GPU side re-runs the probe: tests/test_gpu_dma_probe.py)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import dma_hazard_scan as S
+    findings, cleared = [], []
+    for obj in S.product_objects():
+        f, c = S.classify(S.scan(S.disassemble(obj)))
+        findings += f
+        cleared += c
+    assert not findings, findings[:5]
+    assert all(S.dma_form(h[1]) == "vaddr64" for h in cleared)
+
+
+def test_dma_scanner_flags_the_probe_patterns():
+    """The scanner itself: on the probe kernel's code (every DMA form followed
+    by a ds_read into its address registers) it must report the SADDR and
+    MUBUF sites as findings and the vaddr sites as cleared."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "tools"))
+    import dma_hazard_scan as S
+    hipcc = "/opt/rocm/bin/hipcc"
+    if not os.path.exists(hipcc):
+        pytest.skip("hipcc absent")
+    d = tempfile.mkdtemp()
+    try:
+        out = os.path.join(d, "probe.s")
+        subprocess.run([hipcc, "-O3", "--offload-arch=gfx950", "--cuda-device-only", "-S",
+                        os.path.join(root, "tools", "dma_war_probe.hip"), "-o", out], check=True, capture_output=True)
+        findings, cleared = S.classify(S.scan(open(out).read()))
+    finally:
+        shutil.rmtree(d)
+    assert {S.dma_form(h[1]) for h in findings} == {"saddr", "mubuf"}, findings
+    assert len(cleared) >= 4 and {S.dma_form(h[1]) for h in cleared} == {"vaddr64"}
