@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MDE_ABI_VERSION 6
+#define MDE_ABI_VERSION 7
 
 typedef enum {
   MDE_OK = 0,
@@ -219,6 +219,21 @@ int mde_op_qkv32(const float* a, const float* w, int ldw, const float* bias, int
                  int tokens_pad, float q_scale, float* q, float* k, float* v, void* stream);
 int mde_op_attention32(const float* q, const float* k, const float* v, float* o, int batch, int heads, int tokens,
                        int tokens_pad, int ldo, void* stream);
+/* The exact-fp32 DPT head's kernels (fp32.hip; precision "fp32" engines since ABI 7).  conv3x3_32: out
+ * = act(conv3x3(relu_in ? ReLU(in) : in) + bias) + res0 + res1 over fp32 NHWC maps [batch][h][w][cin]
+ * (cin % 4 == 0), pad 1, stride 1 or 2, weights fp32 [cout_pad][ldw] in (ky, kx, ci) order (ldw % 32
+ * == 0, >= 9 cin rounded up to 32; cout % 4 == 0), res0 / res1 optional maps shaped like out --
+ * reference: DPTHead's resConfUnit / layerN_rn / output_conv convs (upstream dpt.py), the reference's
+ * fp32 TensorRT build (core/common.py:141-144).  conv_transpose32: ConvTranspose2d(k = s = stride)
+ * as a GEMM with a pixel-shuffle epilogue, weights [(dy s + dx) cout + co][ldw] -- DPTHead
+ * resize_layers 0/1.  resize32: bilinear, align_corners=True, fp32 NHWC (c % 4 == 0) --
+ * F.interpolate in FeatureFusionBlock / the head. */
+int mde_op_conv3x3_32(const float* in, int batch, int h, int w, int cin, const float* wt, int ldw, int cout,
+                      int stride, int relu_in, const float* bias, int act, const float* res0, const float* res1,
+                      float* out, void* stream);
+int mde_op_conv_transpose32(const float* in, int batch, int h, int w, int cin, const float* wt, int ldw, int cout,
+                            int stride, const float* bias, float* out, void* stream);
+int mde_op_resize32(const float* in, int batch, int h, int w, int c, int oh, int ow, float* out, void* stream);
 int mde_op_patch_embed(const float* img, int batch, int h, int w, const void* w_f16, int ldw, const float* bias,
                        const float* pos_patch, const float* cls_pos, int dim, void* patch_scratch_f16,
                        float* x32, void* stream);

@@ -121,6 +121,11 @@ PROTOTYPES = {
     "mde_op_qkv32": [c_void_p, c_void_p, c_int, c_void_p, c_int, c_int, c_int, c_int, c_float, c_void_p, c_void_p,
                      c_void_p, c_void_p],
     "mde_op_attention32": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p],
+    "mde_op_conv3x3_32": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                          c_int, c_void_p, c_void_p, c_void_p, c_void_p],
+    "mde_op_conv_transpose32": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_void_p,
+                                c_void_p, c_void_p],
+    "mde_op_resize32": [c_void_p, c_int, c_int, c_int, c_int, c_int, c_int, c_void_p, c_void_p],
     "mde_op_patch_embed": [c_void_p, c_int, c_int, c_int, c_void_p, c_int, c_void_p, c_void_p, c_void_p, c_int,
                            c_void_p, c_void_p, c_void_p],
     "mde_op_conv3x3": [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int, c_int, c_int, c_int, c_void_p,

@@ -368,15 +368,16 @@ hipError_t launch_layernorm(const float* x, h16* y, const float* g, const float*
 }
 
 hipError_t launch_layernorm32(const float* x, float* y, const float* g, const float* b, int rows, int D, float eps,
-                              hipStream_t st) {
+                              hipStream_t st, int T, int skip_cls) {
+  if (T <= 0 || (skip_cls && T < 2)) return hipErrorInvalidValue;
   if (rows <= 0) return hipSuccess;
   const dim3 grid((rows + 3) / 4), block(256);
   switch (D) {
-    case 128: hipLaunchKernelGGL((layernorm_kernel<2, float, float>), grid, block, 0, st, x, y, g, b, rows, eps, 1, 0); break;
-    case 256: hipLaunchKernelGGL((layernorm_kernel<4, float, float>), grid, block, 0, st, x, y, g, b, rows, eps, 1, 0); break;
-    case 384: hipLaunchKernelGGL((layernorm_kernel<6, float, float>), grid, block, 0, st, x, y, g, b, rows, eps, 1, 0); break;
-    case 768: hipLaunchKernelGGL((layernorm_kernel<12, float, float>), grid, block, 0, st, x, y, g, b, rows, eps, 1, 0); break;
-    case 1024: hipLaunchKernelGGL((layernorm_kernel<16, float, float>), grid, block, 0, st, x, y, g, b, rows, eps, 1, 0); break;
+    case 128: hipLaunchKernelGGL((layernorm_kernel<2, float, float>), grid, block, 0, st, x, y, g, b, rows, eps, T, skip_cls); break;
+    case 256: hipLaunchKernelGGL((layernorm_kernel<4, float, float>), grid, block, 0, st, x, y, g, b, rows, eps, T, skip_cls); break;
+    case 384: hipLaunchKernelGGL((layernorm_kernel<6, float, float>), grid, block, 0, st, x, y, g, b, rows, eps, T, skip_cls); break;
+    case 768: hipLaunchKernelGGL((layernorm_kernel<12, float, float>), grid, block, 0, st, x, y, g, b, rows, eps, T, skip_cls); break;
+    case 1024: hipLaunchKernelGGL((layernorm_kernel<16, float, float>), grid, block, 0, st, x, y, g, b, rows, eps, T, skip_cls); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();

@@ -66,23 +66,34 @@ std::string setup_dav2(mde_engine* e) {
   if (c.enc_f32 != 0 && c.enc_f32 != 1) return "bad encoder precision in packed config";
   if (c.enc_f32) need[0] = "patch.w32";
   const char* wsuf = c.enc_f32 ? ".w32" : ".w";  // exact-fp32 encoders carry fp32 linears
+  // exact-fp32 DPT head: fp32 head weights packed (round 5; a round-4 fp32
+  // pack without them keeps the f16 head)
+  e->head_f32 = c.enc_f32 && e->get("head.c1.w32") != nullptr;
+  const char* hsuf = e->head_f32 ? ".w32" : ".w";
+  if (e->head_f32) {
+    if (c.out_channels[0] % 4 || c.out_channels[1] % 4 || c.out_channels[2] % 4 || c.out_channels[3] % 4 ||
+        c.features % 8)
+      return "unsupported DPT channel counts for the fp32 head";
+    for (auto& n : need)
+      if (n == "rs0.w" || n == "rs1.w" || n == "rs3.w" || n == "head.c1.w" || n == "head.c2.w") n += "32";
+  }
   for (int i = 0; i < c.depth; ++i) {
     for (const char* s : {"ln1.g", "ln1.b", "qkv.b", "proj.b", "ls1", "ln2.g", "ln2.b", "fc1.b", "fc2.b", "ls2"})
       need.push_back("b" + std::to_string(i) + "." + s);
     for (const char* s : {"qkv", "proj", "fc1", "fc2"}) need.push_back("b" + std::to_string(i) + "." + s + wsuf);
   }
   for (int i = 0; i < 4; ++i) {
-    need.push_back("proj" + std::to_string(i) + ".w");
+    need.push_back("proj" + std::to_string(i) + hsuf);
     need.push_back("proj" + std::to_string(i) + ".b");
-    need.push_back("rn" + std::to_string(i + 1) + ".w");
+    need.push_back("rn" + std::to_string(i + 1) + hsuf);
   }
   for (int r = 1; r <= 4; ++r) {
     std::string p = "rf" + std::to_string(r) + ".";
-    need.push_back(p + "out.w");
+    need.push_back(p + "out" + hsuf);
     need.push_back(p + "out.b");
     for (int u = 1; u <= 2; ++u)
       for (int cc = 1; cc <= 2; ++cc) {
-        need.push_back(p + "rcu" + std::to_string(u) + ".c" + std::to_string(cc) + ".w");
+        need.push_back(p + "rcu" + std::to_string(u) + ".c" + std::to_string(cc) + hsuf);
         need.push_back(p + "rcu" + std::to_string(u) + ".c" + std::to_string(cc) + ".b");
       }
   }
@@ -213,21 +224,44 @@ size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
   // tap token maps: only without the tap-LayerNorm fold (the projects read
   // the residual stream directly when proj*.wf is packed)
   const bool fold_taps = fold && e.get("proj0.wf");
-  for (int i = 0; i < 4; ++i) t.tap[i] = fold_taps ? nullptr : a.h(bb * np * D);
-  for (int i = 0; i < 4; ++i) t.pj[i] = a.h(bb * np * oc[i]);
-  t.l1 = a.h(bb * s1 * e.c1p);  // channels padded to a multiple of 32 (pad stays 0)
-  t.l2 = a.h(bb * s2 * oc[1]);
-  t.l4 = a.h(bb * s4 * oc[3]);
   const size_t ss[4] = {s1, s2, s3, s4};
-  for (int i = 0; i < 4; ++i) t.rn[i] = a.h(bb * ss[i] * F);
-  t.tb = a.h(bb * s1 * F);
-  t.sb = a.h(bb * s1 * F);
-  t.ub = a.h(bb * s1 * F);
-  t.vb = a.h(bb * s1 * F);
-  t.p4 = a.h(bb * s3 * F);
-  t.p3 = a.h(bb * s2 * F);
-  t.p2 = a.h(bb * s1 * F);
-  t.c1 = a.h(bb * s0 * (F / 2));
+  if (!e.head_f32) {
+    for (int i = 0; i < 4; ++i) t.tap[i] = fold_taps ? nullptr : a.h(bb * np * D);
+    for (int i = 0; i < 4; ++i) t.pj[i] = a.h(bb * np * oc[i]);
+    t.l1 = a.h(bb * s1 * e.c1p);  // channels padded to a multiple of 32 (pad stays 0)
+    t.l2 = a.h(bb * s2 * oc[1]);
+    t.l4 = a.h(bb * s4 * oc[3]);
+    for (int i = 0; i < 4; ++i) t.rn[i] = a.h(bb * ss[i] * F);
+    t.tb = a.h(bb * s1 * F);
+    t.sb = a.h(bb * s1 * F);
+    t.ub = a.h(bb * s1 * F);
+    t.vb = a.h(bb * s1 * F);
+    t.p4 = a.h(bb * s3 * F);
+    t.p3 = a.h(bb * s2 * F);
+    t.p2 = a.h(bb * s1 * F);
+    t.c1 = a.h(bb * s0 * (F / 2));
+  } else {
+    // exact-fp32 DPT head: the same maps in fp32 (l1 unpadded: the fp32 conv
+    // takes any channel count % 4), plus the upsampled head inputs
+    const size_t sout = (size_t)e.cfg.img_h * e.cfg.img_w;
+    for (int i = 0; i < 4; ++i) t.tap32[i] = a.f(bb * np * D);
+    for (int i = 0; i < 4; ++i) t.pj32[i] = a.f(bb * np * oc[i]);
+    t.l1_32 = a.f(bb * s1 * oc[0]);
+    t.l2_32 = a.f(bb * s2 * oc[1]);
+    t.l4_32 = a.f(bb * s4 * oc[3]);
+    for (int i = 0; i < 4; ++i) t.rn32[i] = a.f(bb * ss[i] * F);
+    t.tb32 = a.f(bb * s1 * F);
+    t.sb32 = a.f(bb * s1 * F);
+    t.ub32 = a.f(bb * s1 * F);
+    t.vb32 = a.f(bb * s1 * F);
+    t.p4_32 = a.f(bb * s3 * F);
+    t.p3_32 = a.f(bb * s2 * F);
+    t.p2_32 = a.f(bb * s1 * F);
+    t.up1_32 = a.f(bb * s0 * F);
+    t.c1_32 = a.f(bb * s0 * (F / 2));
+    t.up2_32 = a.f(bb * sout * (F / 2));
+    t.hid32 = a.f(bb * sout * 32);
+  }
   t.ws = h16enc && bb * e.T <= 4096 ? a.f(4 * bb * e.T * D) : nullptr;
   // attention split-KV workspace for the batches whose (head, 128-query)
   // grid is under one workgroup per CU (launch_attention splits those)
@@ -273,6 +307,97 @@ void Runner::dav2_fusion(int r, const h16* x0, const h16* x1, int B, int h, int 
   g.ldo = F;
   gemm((p + ".out").c_str(), g);
   if (dst) step((p + ".resize").c_str(), [&] { return launch_resize(c.b.vb, dst, B, h, w, F, oh, ow, st); });
+}
+
+// The exact-fp32 DPT head (precision "fp32" packs with fp32 head weights):
+// the f16 head's schedule on fp32 maps and the fp32 GEMM (fp32.hip) --
+// projects, resize layers (ConvT pixel shuffle / 3x3 s2), layerN_rn, the
+// four fusion blocks (out_conv before the x2 resize, as the f16 head) and
+// the depth head with its two bilinear upsamples materialised in fp32.
+void Runner::dav2_head32(int B, float* out) {
+  mde_engine& e = *c.e;
+  const PackConfig& cf = e.cfg;
+  const int D = e.D, np = e.np, F = e.F;
+  const int* oc = cf.out_channels;
+  DAV2Buf& b = c.b;
+  const int hs[4] = {4 * e.ph, 2 * e.ph, e.ph, e.h4};
+  const int ws[4] = {4 * e.pw, 2 * e.pw, e.pw, e.w4};
+  const float* lay[4] = {b.l1_32, b.l2_32, b.pj32[2], b.l4_32};
+  char nm[64];
+  for (int i = 0; i < 4; ++i) {
+    {
+      Gemm32Params g = dense32(b.tap32[i], D, "proj" + std::to_string(i) + ".w32", B * np, oc[i], D);
+      g.bias = w32("proj" + std::to_string(i) + ".b");
+      g.out32 = b.pj32[i];
+      g.ldo = oc[i];
+      snprintf(nm, sizeof nm, "reassemble%d.project", i);
+      gemm32(nm, g);
+    }
+    if (i == 0 || i == 1) {
+      const int sc = i == 0 ? 4 : 2;
+      Gemm32Params g = dense32(b.pj32[i], oc[i], i == 0 ? "rs0.w32" : "rs1.w32", B * np, sc * sc * oc[i], oc[i]);
+      g.emode = E_CONVT;
+      g.bias = w32(i == 0 ? "rs0.b" : "rs1.b");
+      g.out32 = i == 0 ? b.l1_32 : b.l2_32;
+      g.s = sc;
+      g.cout = oc[i];
+      g.ldo = oc[i];
+      g.cb = B;
+      g.ih = e.ph;
+      g.iw = e.pw;
+      gemm32(i == 0 ? "reassemble0.convT4" : "reassemble1.convT2", g);
+    } else if (i == 3) {
+      Gemm32Params g = conv32(b.pj32[3], B, e.ph, e.pw, oc[3], "rs3.w32", oc[3], 2);
+      g.bias = w32("rs3.b");
+      g.out32 = b.l4_32;
+      gemm32("reassemble3.conv_s2", g);
+    }
+    Gemm32Params g = conv32(lay[i], B, hs[i], ws[i], oc[i], "rn" + std::to_string(i + 1) + ".w32", F, 1);
+    g.out32 = b.rn32[i];
+    snprintf(nm, sizeof nm, "layer%d_rn", i + 1);
+    gemm32(nm, g);
+  }
+  // fusion: [x0 + RCU1(x1)] -> RCU2 -> out_conv (1x1) -> x2 resize
+  auto fusion = [&](int r, const float* x0, const float* x1, int h, int w, float* dst, int oh, int ow) {
+    const std::string p = "rf" + std::to_string(r);
+    const float* s = x0;
+    if (x1) {
+      rcu32(p + ".rcu1", x1, x0, b.sb32, b.tb32, B, h, w, F);
+      s = b.sb32;
+    }
+    rcu32(p + ".rcu2", s, nullptr, b.ub32, b.tb32, B, h, w, F);
+    Gemm32Params g = dense32(b.ub32, F, p + ".out.w32", B * h * w, F, F);
+    g.bias = w32(p + ".out.b");
+    g.out32 = b.vb32;
+    g.ldo = F;
+    gemm32((p + ".out").c_str(), g);
+    if (dst) step((p + ".resize").c_str(), [&] { return launch_resize32(b.vb32, dst, B, h, w, F, oh, ow, st); });
+  };
+  fusion(4, b.rn32[3], nullptr, hs[3], ws[3], b.p4_32, hs[2], ws[2]);
+  fusion(3, b.p4_32, b.rn32[2], hs[2], ws[2], b.p3_32, hs[1], ws[1]);
+  fusion(2, b.p3_32, b.rn32[1], hs[1], ws[1], b.p2_32, hs[0], ws[0]);
+  fusion(1, b.p2_32, b.rn32[0], hs[0], ws[0], nullptr, 0, 0);  // 1x1 result in vb32 at hs[0] x ws[0]
+  // head: x2 upsample -> output_conv1 -> upsample to the input size ->
+  // output_conv2 (3x3 + ReLU, then 1x1 + activation)
+  const int H1 = 2 * hs[0], W1 = 2 * ws[0], OH = cf.img_h, OW = cf.img_w;
+  step("head.upsample1", [&] { return launch_resize32(b.vb32, b.up1_32, B, hs[0], ws[0], F, H1, W1, st); });
+  {
+    Gemm32Params g = conv32(b.up1_32, B, H1, W1, F, "head.c1.w32", F / 2, 1);
+    g.bias = w32("head.c1.b");
+    g.out32 = b.c1_32;
+    gemm32("head.output_conv1", g);
+  }
+  step("head.upsample2", [&] { return launch_resize32(b.c1_32, b.up2_32, B, H1, W1, F / 2, OH, OW, st); });
+  {
+    Gemm32Params g = conv32(b.up2_32, B, OH, OW, F / 2, "head.c2.w32", cf.head_hidden, 1);
+    g.bias = w32("head.c2.b");
+    g.act = ACT_RELU;
+    g.out32 = b.hid32;
+    gemm32("head.output_conv2", g);
+  }
+  step("head.output_conv3", [&] {
+    return launch_head32(b.hid32, w32("head.c3.w"), e.head_b2, B * OH * OW, cf.metric, cf.max_depth, out, st);
+  });
 }
 
 hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
@@ -459,8 +584,15 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
       }
       if (tap < 4 && cf.taps[tap] == i) {
         snprintf(nm, sizeof nm, "tap%d.norm", tap);
-        h16* dst = b.tap[tap];
-        step(nm, [&] { return launch_layernorm(b.X, dst, w32("norm.g"), w32("norm.b"), B * T, D, cf.ln_eps, T, 1, st); });
+        if (e.head_f32) {
+          float* dst = b.tap32[tap];
+          step(nm, [&] {
+            return launch_layernorm32(b.X, dst, w32("norm.g"), w32("norm.b"), B * T, D, cf.ln_eps, st, T, 1);
+          });
+        } else {
+          h16* dst = b.tap[tap];
+          step(nm, [&] { return launch_layernorm(b.X, dst, w32("norm.g"), w32("norm.b"), B * T, D, cf.ln_eps, T, 1, st); });
+        }
         ++tap;
       }
     }
@@ -582,6 +714,10 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
   }
   }  // f16 encoder
   if (tap != 4) return hipErrorInvalidValue;
+  if (e.head_f32) {
+    dav2_head32(B, out);
+    return err;
+  }
   for (int i = 0; i < 4; ++i) reassemble(i);
   // ---- fusion (refinenet4 .. refinenet1) ----
   dav2_fusion(4, b.rn[3], nullptr, B, hs[3], ws[3], b.p4, hs[2], ws[2]);
@@ -1394,6 +1530,67 @@ int mde_op_linear32(const float* a, int lda, const float* w, int ldw, int m, int
   g.out32 = out;
   g.ldo = ldo;
   OP_RET(launch_gemm32(g, (hipStream_t)st), "linear32");
+}
+
+int mde_op_conv3x3_32(const float* in, int batch, int h, int w, int cin, const float* wt, int ldw, int cout,
+                      int stride, int relu_in, const float* bias, int act, const float* res0, const float* res1,
+                      float* out, void* st) {
+  if (!in || !wt || !out) return fail(MDE_ERR_ARG, "null argument");
+  if (stride != 1 && stride != 2) return fail(MDE_ERR_ARG, "stride must be 1 or 2");
+  if (batch <= 0 || h <= 0 || w <= 0 || cin <= 0 || cout <= 0) return fail(MDE_ERR_ARG, "bad shape");
+  Gemm32Params g;
+  g.amode = A_CONV3;
+  g.emode = E_STORE;
+  g.A = in;
+  g.cb = batch;
+  g.ch = h;
+  g.cw = w;
+  g.cc = cin;
+  g.stride = stride;
+  g.oh = (h - 1) / stride + 1;
+  g.ow = (w - 1) / stride + 1;
+  g.W = wt;
+  g.ldw = ldw;
+  g.M = batch * g.oh * g.ow;
+  g.N = cout;
+  g.K = 9 * cin;
+  g.relu_in = relu_in;
+  g.bias = bias;
+  g.act = act;
+  g.res0 = res0;
+  g.res1 = res1;
+  g.out32 = out;
+  g.ldo = cout;
+  OP_RET(launch_gemm32(g, (hipStream_t)st), "conv3x3_32");
+}
+
+int mde_op_conv_transpose32(const float* in, int batch, int h, int w, int cin, const float* wt, int ldw, int cout,
+                            int stride, const float* bias, float* out, void* st) {
+  if (!in || !wt || !out) return fail(MDE_ERR_ARG, "null argument");
+  if (batch <= 0 || h <= 0 || w <= 0 || stride < 1) return fail(MDE_ERR_ARG, "bad shape");
+  Gemm32Params g;
+  g.emode = E_CONVT;
+  g.A = in;
+  g.lda = cin;
+  g.W = wt;
+  g.ldw = ldw;
+  g.M = batch * h * w;
+  g.N = stride * stride * cout;
+  g.K = cin;
+  g.bias = bias;
+  g.out32 = out;
+  g.ldo = cout;
+  g.s = stride;
+  g.cout = cout;
+  g.cb = batch;
+  g.ih = h;
+  g.iw = w;
+  OP_RET(launch_gemm32(g, (hipStream_t)st), "conv_transpose32");
+}
+
+int mde_op_resize32(const float* in, int batch, int h, int w, int c, int oh, int ow, float* out, void* st) {
+  if (!in || !out) return fail(MDE_ERR_ARG, "null argument");
+  OP_RET(launch_resize32(in, out, batch, h, w, c, oh, ow, (hipStream_t)st), "resize32");
 }
 
 int mde_op_linear_residual32(const float* a, int lda, const float* w, int ldw, int m, int n, int k,

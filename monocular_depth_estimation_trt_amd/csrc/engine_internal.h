@@ -43,6 +43,11 @@ struct DAV2Buf {
   // exact-fp32 encoder (PackConfig::enc_f32, fp32.hip): fp32 patch rows, LN
   // output, q / k / v [B*H][Tpad][64], attention output, MLP hidden (else null)
   float *P32, *Hn32, *Q32, *K32, *V32, *O32, *Mh32;
+  // exact-fp32 DPT head (packs with head.c1.w32, fp32.hip): fp32 NHWC maps
+  // mirroring the f16 ones above, the x2-upsampled fusion output, output_conv1,
+  // its upsample to the input size and the head's hidden map (else null)
+  float *tap32[4], *pj32[4], *l1_32, *l2_32, *l4_32, *rn32[4];
+  float *tb32, *sb32, *ub32, *vb32, *p4_32, *p3_32, *p2_32, *up1_32, *c1_32, *up2_32, *hid32;
 };
 
 // fp32 elements of a context's E_STORE split-K workspace (launch_gemm bounds
@@ -99,6 +104,7 @@ struct mde_engine {
   int ph = 0, pw = 0, np = 0, T = 0, Tpad = 0, D = 0, H = 0, F = 0;
   int h4 = 0, w4 = 0;
   int c1p = 0;          // reassemble-0 channels padded to a multiple of 32 (direct-conv input)
+  bool head_f32 = false;  // DA-V2 exact-fp32 DPT head (fp32 head weights packed, precision "fp32")
   float head_b2 = 0.f;  // final 1x1 conv bias (scalar kernel argument; both families)
   // Depth Pro geometry: G tokens per side of a 384^2 patch, pyramid levels
   int G = 0, nseq = 0;  // nseq = patches per image (35)
@@ -289,6 +295,44 @@ struct Runner {
   void gemm32(const char* name, const Gemm32Params& g) {
     step(name, [&] { return launch_gemm32(g, st); });
   }
+  // exact-fp32 3x3 pad-1 conv over an fp32 NHWC map [B][h][w][cin] (implicit im2col)
+  Gemm32Params conv32(const float* in, int B, int h, int w, int cin, const std::string& wn, int cout, int stride) {
+    Gemm32Params g;
+    g.amode = A_CONV3;
+    g.emode = E_STORE;
+    g.A = in;
+    g.cb = B;
+    g.ch = h;
+    g.cw = w;
+    g.cc = cin;
+    g.stride = stride;
+    g.oh = (h - 1) / stride + 1;
+    g.ow = (w - 1) / stride + 1;
+    g.W = w32(wn);
+    g.ldw = ldw(wn);
+    g.M = B * g.oh * g.ow;
+    g.N = cout;
+    g.K = 9 * cin;
+    g.ldo = cout;
+    return g;
+  }
+  // the fp32 pre-activation residual conv unit (rcu below, on fp32 maps)
+  void rcu32(const std::string& pfx, const float* x, const float* extra, float* out, float* tmp, int B, int h, int w,
+             int F) {
+    Gemm32Params g1 = conv32(x, B, h, w, F, pfx + ".c1.w32", F, 1);
+    g1.relu_in = 1;
+    g1.bias = w32_opt(pfx + ".c1.b");
+    g1.act = ACT_RELU;
+    g1.out32 = tmp;
+    gemm32((pfx + ".c1").c_str(), g1);
+    Gemm32Params g2 = conv32(tmp, B, h, w, F, pfx + ".c2.w32", F, 1);
+    g2.bias = w32_opt(pfx + ".c2.b");
+    g2.res0 = x;
+    g2.res1 = extra;
+    g2.out32 = out;
+    gemm32((pfx + ".c2").c_str(), g2);
+  }
+  void dav2_head32(int B, float* out);
 
   void gemm(const char* name, const GemmParams& g) {
     GemmParams q = g;

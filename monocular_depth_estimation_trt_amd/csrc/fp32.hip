@@ -9,16 +9,25 @@
 // hidden layer all fp32 (23-bit mantissa, fp32 range) -- on gfx950's exact
 // fp32 matrix instructions (v_mfma_f32_16x16x4_f32 / v_mfma_f32_32x32x2_f32,
 // MI355X_MICROARCH.md: 157 TF/s, the fp32 vector rate, bit-equal to an fmaf
-// chain).  The DPT head stays on the f16 kernels: its inputs are the taps'
-// LayerNorm outputs, bounded by the norm.
+// chain).  Since round 5 the DPT head of such an engine is fp32 too (packs
+// with the fp32 head weights, `head.c1.w32`): projects, resize layers,
+// layerN_rn, the fusion blocks and the depth head on fp32 maps, as the
+// reference's fp32 TensorRT engine runs every layer in fp32
+// (reports/tune/fp32_depth_anything_v2.json: 'Float': 188 layers).
 //
-//   gemm32_kernel     C = A W^T, A fp32 [M][lda], W fp32 [Npad][ldw]; epilogues
-//                     E_STORE (fp32 or f16 out, bias, ReLU / GELU), E_QKV
-//                     (fp32 q / k / v [B*H][Tpad][64], q scaled), E_RESID
-//                     (x32 += ls * (acc + bias)), E_PATCH (x32 rows = acc +
-//                     bias + pos)
+//   gemm32_kernel     C = A W^T, W fp32 [Npad][ldw]; A fp32 [M][lda] (A_DENSE)
+//                     or the implicit im2col of a 3x3 pad-1 conv over an fp32
+//                     NHWC map (A_CONV3, optional ReLU on the operand);
+//                     epilogues E_STORE (fp32 or f16 out, bias, ReLU / GELU,
+//                     two residual maps), E_QKV (fp32 q / k / v
+//                     [B*H][Tpad][64], q scaled), E_RESID (x32 += ls * (acc +
+//                     bias)), E_PATCH (x32 rows = acc + bias + pos), E_CONVT
+//                     (ConvTranspose k = s pixel shuffle)
 //   attn32_kernel     softmax(q k^T) v over those fp32 rows, online softmax in
 //                     log2 units (q carries dh^-0.5 * log2 e), fp32 out
+//   resize32_kernel   bilinear align_corners=True over fp32 NHWC maps
+//   head32_kernel     output_conv2's last 1x1 conv + activation over the
+//                     fp32 hidden map
 //
 // The GEMM keeps the f16 kernel's LDS geometry (gemm.hip): 128-B rows (here 32
 // floats, one K-step), chunk swizzle c ^ (row & 7) applied on the global_load_lds
@@ -44,7 +53,11 @@ MDE_DEV void wait_vm32() { asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); }
 
 MDE_DEV int pch32(int r, int lc) { return lc ^ (r & 7); }
 
-template <int BM, int BN, int EM>
+// padding taps of the implicit-im2col A read this (a glds lane cannot be
+// masked, it can be redirected)
+__device__ __attribute__((aligned(16))) float g_zero32[4];
+
+template <int BM, int BN, int EM, int AM>
 __global__ void __launch_bounds__(256) gemm32_kernel(const Gemm32Params p) {
   constexpr int WM = 2, WN = 2, NW = 4;
   constexpr int TM = BM / (WM * 16), TN = BN / (WN * 16);
@@ -66,22 +79,60 @@ __global__ void __launch_bounds__(256) gemm32_kernel(const Gemm32Params p) {
   const int lrow = lane / CH;
   const int lch = pch32(lrow, lane % CH);
   const float* arow[APASS];
+  int iy0[APASS], ix0[APASS];
+  bool rv[APASS];
 #pragma unroll
   for (int i = 0; i < APASS; ++i) {
     const int gm = m0 + (wave + i * NW) * RW + lrow;
-    arow[i] = p.A + (size_t)(gm < p.M ? gm : p.M - 1) * p.lda + lch * 4;
+    rv[i] = gm < p.M;
+    const int gmc = rv[i] ? gm : p.M - 1;
+    if constexpr (AM == A_DENSE) {
+      arow[i] = p.A + (size_t)gmc * p.lda + lch * 4;
+      iy0[i] = ix0[i] = 0;
+    } else {  // output pixel (b, oy, ox) of row gm
+      const int hw = p.oh * p.ow;
+      const int b = gmc / hw, rem = gmc - (gmc / hw) * hw;
+      const int oy = rem / p.ow, ox = rem - (rem / p.ow) * p.ow;
+      iy0[i] = oy * p.stride - 1;
+      ix0[i] = ox * p.stride - 1;
+      arow[i] = p.A + (size_t)b * p.ch * p.cw * p.cc;
+    }
   }
   const float* wrow = p.W + (size_t)(n0 + wave * RW + lrow) * p.ldw + lch * 4;
   const int nk = (p.K + 31) / 32;
+  // A_CONV3: this lane's chunk at K-step kt is k = 32 kt + 4 lch = tap * cc + c
+  // (cc % 4 == 0: a chunk never straddles taps), advanced by 32 per step
+  int tap = 0, cch = lch * 4;
+  if constexpr (AM == A_CONV3) {
+    tap = cch / p.cc;
+    cch -= tap * p.cc;
+  }
 
   auto issue = [&](int kt, int buf) {
     char* sb = smem + buf * STAGE;
     const int k0 = kt * 32;
-    // K tail: W is zero-padded to ldw; a lane whose chunk lies past K reads
-    // column 0 of its row instead (finite, and inside the row even when K < 32)
-    const int ka = k0 + lch * 4 < p.K ? k0 : -lch * 4;
+    if constexpr (AM == A_DENSE) {
+      // K tail: W is zero-padded to ldw; a lane whose chunk lies past K reads
+      // column 0 of its row instead (finite, and inside the row even when K < 32)
+      const int ka = k0 + lch * 4 < p.K ? k0 : -lch * 4;
 #pragma unroll
-    for (int i = 0; i < APASS; ++i) glds16f(arow[i] + ka, sb + (wave + i * NW) * RW * ROWB);
+      for (int i = 0; i < APASS; ++i) glds16f(arow[i] + ka, sb + (wave + i * NW) * RW * ROWB);
+    } else {
+      const bool kv = k0 + lch * 4 < p.K;
+      const int ky = tap / 3, kx = tap - (tap / 3) * 3;
+#pragma unroll
+      for (int i = 0; i < APASS; ++i) {
+        const int iy = iy0[i] + ky, ix = ix0[i] + kx;
+        const bool ok = rv[i] && kv && iy >= 0 && iy < p.ch && ix >= 0 && ix < p.cw;
+        const float* src = ok ? arow[i] + ((size_t)iy * p.cw + ix) * p.cc + cch : g_zero32;
+        glds16f(src, sb + (wave + i * NW) * RW * ROWB);
+      }
+      cch += 32;
+      while (cch >= p.cc) {
+        cch -= p.cc;
+        ++tap;
+      }
+    }
 #pragma unroll
     for (int i = 0; i < BPASS; ++i)
       glds16f(wrow + (size_t)i * NW * RW * p.ldw + k0, sb + BM * ROWB + (wave + i * NW) * RW * ROWB);
@@ -104,6 +155,12 @@ __global__ void __launch_bounds__(256) gemm32_kernel(const Gemm32Params p) {
       for (int i = 0; i < TM; ++i) {
         const int r = wm * TM * 16 + i * 16 + (lane & 15);
         fa[i] = *reinterpret_cast<const f32x4*>(sA + r * ROWB + pch32(r, lc) * 16);
+        if constexpr (AM == A_CONV3) {
+          if (p.relu_in) {
+#pragma unroll
+            for (int t = 0; t < 4; ++t) fa[i][t] = fa[i][t] > 0.f ? fa[i][t] : 0.f;
+          }
+        }
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
@@ -140,7 +197,7 @@ __global__ void __launch_bounds__(256) gemm32_kernel(const Gemm32Params p) {
       const int n = n0 + wn * TN * 16 + j * 16 + (lane >> 4) * 4;
       if (n >= p.N) continue;
       f32x4 v = acc[i][j];
-      if (p.bias) {
+      if (EM != E_CONVT && p.bias) {
         const float4 b = *reinterpret_cast<const float4*>(p.bias + n);
         v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
       }
@@ -151,6 +208,14 @@ __global__ void __launch_bounds__(256) gemm32_kernel(const Gemm32Params p) {
         } else if (p.act == ACT_GELU) {
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = 0.5f * v[r] * (1.f + erff(v[r] * 0.70710678118654752f));
+        }
+        if (p.res0) {
+          const float4 r = *reinterpret_cast<const float4*>(p.res0 + (size_t)m * p.ldo + n);
+          v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+        }
+        if (p.res1) {
+          const float4 r = *reinterpret_cast<const float4*>(p.res1 + (size_t)m * p.ldo + n);
+          v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
         }
         if (p.out32) {
           *reinterpret_cast<float4*>(p.out32 + (size_t)m * p.ldo + n) = make_float4(v[0], v[1], v[2], v[3]);
@@ -172,6 +237,17 @@ __global__ void __launch_bounds__(256) gemm32_kernel(const Gemm32Params p) {
         const float4 ps = *reinterpret_cast<const float4*>(p.pos + (size_t)pi * p.ldo + n);
         *reinterpret_cast<float4*>(p.x32 + ((size_t)b * p.T + 1 + pi) * p.ldo + n) =
             make_float4(v[0] + ps.x, v[1] + ps.y, v[2] + ps.z, v[3] + ps.w);
+      } else if constexpr (EM == E_CONVT) {
+        // cout % 4 == 0: the lane's four columns are four channels of one (dy, dx)
+        const int hw = p.ih * p.iw;
+        const int b = m / hw, rem = m - (m / hw) * hw;
+        const int iy = rem / p.iw, ix = rem - (rem / p.iw) * p.iw;
+        const int q = n / p.cout, co = n - (n / p.cout) * p.cout;
+        const int dy = q / p.s, dx = q - (q / p.s) * p.s;
+        const float4 bb = p.bias ? *reinterpret_cast<const float4*>(p.bias + co) : make_float4(0.f, 0.f, 0.f, 0.f);
+        const size_t px = ((size_t)b * p.ih * p.s + (size_t)iy * p.s + dy) * ((size_t)p.iw * p.s) + (size_t)ix * p.s + dx;
+        *reinterpret_cast<float4*>(p.out32 + px * p.ldo + co) =
+            make_float4(v[0] + bb.x, v[1] + bb.y, v[2] + bb.z, v[3] + bb.w);
       } else if constexpr (EM == E_QKV) {
         const int D = p.heads * 64;
         const int which = n / D, hn = n - which * D, h = hn >> 6, d = hn & 63;
@@ -190,11 +266,17 @@ hipError_t run32(const Gemm32Params& p, hipStream_t st) {
   const long long tiles = (long long)((p.M + BM - 1) / BM) * ((p.N + BN - 1) / BN);
   if (tiles <= 0) return hipSuccess;
   const dim3 grid((unsigned)tiles), block(256);
+  if (p.amode == A_CONV3) {
+    if (p.emode != E_STORE) return hipErrorInvalidValue;
+    hipLaunchKernelGGL((gemm32_kernel<BM, BN, E_STORE, A_CONV3>), grid, block, 0, st, p);
+    return hipGetLastError();
+  }
   switch (p.emode) {
-    case E_STORE: hipLaunchKernelGGL((gemm32_kernel<BM, BN, E_STORE>), grid, block, 0, st, p); break;
-    case E_QKV: hipLaunchKernelGGL((gemm32_kernel<BM, BN, E_QKV>), grid, block, 0, st, p); break;
-    case E_RESID: hipLaunchKernelGGL((gemm32_kernel<BM, BN, E_RESID>), grid, block, 0, st, p); break;
-    case E_PATCH: hipLaunchKernelGGL((gemm32_kernel<BM, BN, E_PATCH>), grid, block, 0, st, p); break;
+    case E_STORE: hipLaunchKernelGGL((gemm32_kernel<BM, BN, E_STORE, A_DENSE>), grid, block, 0, st, p); break;
+    case E_QKV: hipLaunchKernelGGL((gemm32_kernel<BM, BN, E_QKV, A_DENSE>), grid, block, 0, st, p); break;
+    case E_RESID: hipLaunchKernelGGL((gemm32_kernel<BM, BN, E_RESID, A_DENSE>), grid, block, 0, st, p); break;
+    case E_PATCH: hipLaunchKernelGGL((gemm32_kernel<BM, BN, E_PATCH, A_DENSE>), grid, block, 0, st, p); break;
+    case E_CONVT: hipLaunchKernelGGL((gemm32_kernel<BM, BN, E_CONVT, A_DENSE>), grid, block, 0, st, p); break;
     default: return hipErrorInvalidValue;
   }
   return hipGetLastError();
@@ -390,17 +472,101 @@ attn32_kernel(const float* __restrict__ q, const float* __restrict__ k, const fl
                       acc[db][4 * g4 + 3] * inv);
 }
 
+// fp32 NHWC bilinear resize, align_corners=True (PyTorch's index math,
+// mde_device.h ac_index); one thread per (pixel, 4 channels)
+__global__ void __launch_bounds__(256) resize32_kernel(const float* __restrict__ in, float* __restrict__ out, int ih,
+                                                       int iw, int C4, int oh, int ow, long long n) {
+  const long long id = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (id >= n) return;
+  const int c4 = (int)(id % C4);
+  long long pix = id / C4;
+  const int ox = (int)(pix % ow);
+  pix /= ow;
+  const int oy = (int)(pix % oh);
+  const int b = (int)(pix / oh);
+  int y0, y1, x0, x1;
+  float ly0, ly1, lx0, lx1;
+  ac_index(ac_scale(ih, oh), oy, ih, y0, y1, ly0, ly1);
+  ac_index(ac_scale(iw, ow), ox, iw, x0, x1, lx0, lx1);
+  const size_t C = (size_t)C4 * 4;
+  const float* base = in + (size_t)b * ih * iw * C + c4 * 4;
+  const float4 a = *reinterpret_cast<const float4*>(base + ((size_t)y0 * iw + x0) * C);
+  const float4 bb = *reinterpret_cast<const float4*>(base + ((size_t)y0 * iw + x1) * C);
+  const float4 c = *reinterpret_cast<const float4*>(base + ((size_t)y1 * iw + x0) * C);
+  const float4 d = *reinterpret_cast<const float4*>(base + ((size_t)y1 * iw + x1) * C);
+  float4 v;
+  v.x = ly0 * (lx0 * a.x + lx1 * bb.x) + ly1 * (lx0 * c.x + lx1 * d.x);
+  v.y = ly0 * (lx0 * a.y + lx1 * bb.y) + ly1 * (lx0 * c.y + lx1 * d.y);
+  v.z = ly0 * (lx0 * a.z + lx1 * bb.z) + ly1 * (lx0 * c.z + lx1 * d.z);
+  v.w = ly0 * (lx0 * a.w + lx1 * bb.w) + ly1 * (lx0 * c.w + lx1 * d.w);
+  *reinterpret_cast<float4*>(out + (size_t)id * 4) = v;
+}
+
+// output_conv2's last 1x1 conv (32 -> 1) + activation over the ReLU'd fp32
+// hidden map; one thread per pixel (the E_HEAD epilogue's arithmetic)
+__global__ void __launch_bounds__(256) head32_kernel(const float* __restrict__ hid, const float* __restrict__ w2,
+                                                     float b2, int M, int metric, float max_depth,
+                                                     float* __restrict__ out) {
+  const int m = blockIdx.x * 256 + threadIdx.x;
+  if (m >= M) return;
+  const float4* h = reinterpret_cast<const float4*>(hid + (size_t)m * 32);
+  float z = 0.f;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const float4 v = h[j];
+    z += v.x * w2[4 * j] + v.y * w2[4 * j + 1] + v.z * w2[4 * j + 2] + v.w * w2[4 * j + 3];
+  }
+  z += b2;
+  out[m] = metric == 2 ? __expf(z) : metric ? max_depth / (1.f + __expf(-z)) : (z > 0.f ? z : 0.f);
+}
+
 }  // namespace
+
+hipError_t launch_resize32(const float* in, float* out, int B, int ih, int iw, int C, int oh, int ow, hipStream_t st) {
+  if (B <= 0) return hipSuccess;
+  if (!in || !out || ih <= 0 || iw <= 0 || oh <= 0 || ow <= 0 || C <= 0 || (C & 3) || ((uintptr_t)in & 15) ||
+      ((uintptr_t)out & 15))
+    return hipErrorInvalidValue;
+  const long long n = (long long)B * oh * ow * (C / 4);
+  hipLaunchKernelGGL(resize32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, in, out, ih, iw, C / 4, oh,
+                     ow, n);
+  return hipGetLastError();
+}
+
+hipError_t launch_head32(const float* hid, const float* w2, float b2, int M, int metric, float max_depth, float* out,
+                         hipStream_t st) {
+  if (M <= 0) return hipSuccess;
+  if (!hid || !w2 || !out || ((uintptr_t)hid & 15)) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(head32_kernel, dim3((unsigned)((M + 255) / 256)), dim3(256), 0, st, hid, w2, b2, M, metric,
+                     max_depth, out);
+  return hipGetLastError();
+}
 
 hipError_t launch_gemm32(const Gemm32Params& p, hipStream_t st) {
   if (p.M <= 0 || p.N <= 0) return hipSuccess;
-  if (p.K <= 0 || (p.K & 3) || (p.N & 3) || (p.ldw & 31) || p.ldw < ((p.K + 31) / 32) * 32 || (p.lda & 3) ||
-      p.lda < p.K || !p.A || !p.W)
+  if (p.K <= 0 || (p.K & 3) || (p.N & 3) || (p.ldw & 31) || p.ldw < ((p.K + 31) / 32) * 32 || !p.A || !p.W)
     return hipErrorInvalidValue;
+  if (p.amode == A_DENSE) {
+    if ((p.lda & 3) || p.lda < p.K) return hipErrorInvalidValue;
+  } else if (p.amode == A_CONV3) {
+    // the grid assumes M = cb * oh * ow output pixels of a 3x3 pad-1 conv
+    if (p.cc <= 0 || (p.cc & 3) || p.K != 9 * p.cc || p.cb <= 0 || p.ch <= 0 || p.cw <= 0 || p.stride < 1 ||
+        p.oh != (p.ch - 1) / p.stride + 1 || p.ow != (p.cw - 1) / p.stride + 1 || p.M != p.cb * p.oh * p.ow ||
+        p.emode != E_STORE)
+      return hipErrorInvalidValue;
+  } else {
+    return hipErrorInvalidValue;
+  }
   if (((uintptr_t)p.A & 15) || ((uintptr_t)p.W & 15)) return hipErrorInvalidValue;
   switch (p.emode) {
     case E_STORE:
-      if ((p.out32 == nullptr) == (p.out16 == nullptr) || (p.ldo & 3)) return hipErrorInvalidValue;
+      if ((p.out32 == nullptr) == (p.out16 == nullptr) || (p.ldo & 3) || p.ldo < p.N) return hipErrorInvalidValue;
+      if ((p.res0 || p.res1) && !p.out32) return hipErrorInvalidValue;
+      break;
+    case E_CONVT:
+      if (!p.out32 || p.s < 1 || p.cout <= 0 || (p.cout & 3) || p.N != p.s * p.s * p.cout || p.ih <= 0 ||
+          p.iw <= 0 || p.cb <= 0 || p.M != p.cb * p.ih * p.iw || (p.ldo & 3) || p.ldo < p.cout)
+        return hipErrorInvalidValue;
       break;
     case E_RESID:
       if (!p.x32 || !p.ls || (p.ldo & 3)) return hipErrorInvalidValue;

@@ -99,6 +99,7 @@ struct GemmParams {
 //   E_PATCH  x32[(b*T + 1 + p)*ldo + n] = acc + bias[n] + pos[p*ldo + n]
 struct Gemm32Params {
   int emode = E_STORE;
+  int amode = A_DENSE;  // A_DENSE or A_CONV3 (implicit im2col of a 3x3 pad-1 conv over an fp32 NHWC map)
   int M = 0, N = 0, K = 0;
   const float* A = nullptr; int lda = 0;
   const float* W = nullptr; int ldw = 0;
@@ -107,8 +108,24 @@ struct Gemm32Params {
   float* x32 = nullptr; const float* ls = nullptr;
   float *q = nullptr, *k = nullptr, *v = nullptr; int T = 0, Tpad = 0, heads = 0; float qscale = 1.f;
   const float* pos = nullptr; int npatch = 0;
+  // A_CONV3: input map [cb][ch][cw][cc] (cc % 4 == 0), output [cb][oh][ow],
+  // K = 9 cc in (ky, kx, c) order; relu_in: ReLU applied to the A operand
+  int cb = 0, ch = 0, cw = 0, cc = 0, stride = 1, oh = 0, ow = 0, relu_in = 0;
+  // E_STORE: out = act(acc + bias) + res0 + res1 (fp32 maps laid out like out32)
+  const float* res0 = nullptr; const float* res1 = nullptr;
+  // E_CONVT (ConvTranspose k = s): rows = input pixels [cb][ih][iw], column
+  // n = (dy s + dx) cout + co -> out32 pixel (s iy + dy, s ix + dx), channel co
+  // (stride ldo), + bias[co]
+  int s = 0, cout = 0, ih = 0, iw = 0;
 };
 hipError_t launch_gemm32(const Gemm32Params& p, hipStream_t st);
+// fp32 NHWC bilinear resize, align_corners=True ([B][ih][iw][C] -> [B][oh][ow][C], C % 4 == 0)
+hipError_t launch_resize32(const float* in, float* out, int B, int ih, int iw, int C, int oh, int ow, hipStream_t st);
+// DPT head tail over an fp32 hidden map hid [M][32] (already ReLU'd): out[m] =
+// act(sum_c w2[c] hid[m][c] + b2), act = ReLU (relative), sigmoid * max_depth
+// (metric, 1), exp (2) -- output_conv2's last 1x1 conv and activation
+hipError_t launch_head32(const float* hid, const float* w2, float b2, int M, int metric, float max_depth, float* out,
+                         hipStream_t st);
 // fp32 attention over q (pre-scaled by dh^-0.5 * log2 e) / k / v fp32
 // [B*H][Tpad][64] rows -> o fp32 [B*T][ldo], head h in columns 64h .. 64h+63
 hipError_t launch_attention32(const float* q, const float* k, const float* v, float* o, int B, int H, int T,
@@ -163,8 +180,10 @@ hipError_t launch_patch_prep(const float* img, h16* P, float* X, const float* cl
                              int W, int ph, int pw, int T, int D, hipStream_t st, h16* Xh = nullptr,
                              float* lnst = nullptr, const float* cls_st = nullptr, float* P32 = nullptr);
 // fp32 rows -> LayerNorm -> fp32 rows (exact-fp32 engines)
+// (T, skip_cls = 1: the cls row of every T-row sequence dropped, the patch
+// rows written as the [B*(T-1)][D] NHWC token map -- the taps' final norm)
 hipError_t launch_layernorm32(const float* x, float* y, const float* g, const float* b, int rows, int D, float eps,
-                              hipStream_t st);
+                              hipStream_t st, int T = 1, int skip_cls = 0);
 
 hipError_t launch_resize(const h16* in, h16* out, int B, int ih, int iw, int C, int oh, int ow,
                          hipStream_t st);

@@ -76,6 +76,21 @@ def _convT(w: np.ndarray) -> np.ndarray:
     return _pad2(np.ascontiguousarray(w.transpose(2, 3, 1, 0)).reshape(s * s * co, ci))
 
 
+def _conv3_f32(w: np.ndarray) -> np.ndarray:
+    """[Cout][Cin][3][3] -> fp32 [Cout_pad][9*Cin pad32] in (ky, kx, ci) order:
+    the exact-fp32 implicit-im2col conv's weight operand (csrc/fp32.hip)."""
+    co, ci, kh, kw = w.shape
+    assert kh == 3 and kw == 3, w.shape
+    return _pad2_f32(np.ascontiguousarray(w.transpose(0, 2, 3, 1)).reshape(co, 9 * ci))
+
+
+def _convT_f32(w: np.ndarray) -> np.ndarray:
+    """ConvTranspose2d weight [Cin][Cout][s][s] (k == s) -> fp32 [(dy*s+dx)*Cout+co][Cin]."""
+    ci, co, s, s2 = w.shape
+    assert s == s2
+    return _pad2_f32(np.ascontiguousarray(w.transpose(2, 3, 1, 0)).reshape(s * s * co, ci))
+
+
 def interpolate_pos_embed(pos: np.ndarray, ph: int, pw: int) -> np.ndarray:
     """Upstream DINOv2 interpolate_pos_encoding (bicubic, scale_factor with the
     0.1 offset, antialias False).  [1, 1+M*M, D] -> [1, 1+ph*pw, D] fp32."""
@@ -190,6 +205,11 @@ def packed_tensors(sd: Dict[str, np.ndarray], cfg: dict, img_h: int, img_w: int,
     o["norm.g"] = f32(sd[p + "norm.weight"])
     o["norm.b"] = f32(sd[p + "norm.bias"])
     h = "depth_head."
+    if enc_f32:
+        # the exact-fp32 engine's DPT head: every conv / linear weight fp32
+        # (`*.w32`), the head run on fp32 maps (engine.hip dav2_head32)
+        _head_f32(sd, cfg, o, f32)
+        return o
     for i in range(4):
         w = sd[f"{h}projects.{i}.weight"]
         o[f"proj{i}.w"] = _pad2(w.reshape(w.shape[0], w.shape[1]))
@@ -224,6 +244,40 @@ def packed_tensors(sd: Dict[str, np.ndarray], cfg: dict, img_h: int, img_w: int,
     o["head.c3.w"] = f32(sd[s + "output_conv2.2.weight"])
     o["head.c3.b"] = f32(sd[s + "output_conv2.2.bias"])
     return o
+
+
+def _head_f32(sd, cfg, o, f32) -> None:
+    """fp32 DPT head weights: the f16 head's tensors under `.w32` names, no
+    channel padding (the fp32 conv takes any channel count % 4)."""
+    h = "depth_head."
+    for i in range(4):
+        w = sd[f"{h}projects.{i}.weight"]
+        o[f"proj{i}.w32"] = _pad2_f32(w.reshape(w.shape[0], w.shape[1]))
+        o[f"proj{i}.b"] = f32(sd[f"{h}projects.{i}.bias"])
+    o["rs0.w32"] = _convT_f32(sd[h + "resize_layers.0.weight"])
+    o["rs0.b"] = f32(sd[h + "resize_layers.0.bias"])
+    o["rs1.w32"] = _convT_f32(sd[h + "resize_layers.1.weight"])
+    o["rs1.b"] = f32(sd[h + "resize_layers.1.bias"])
+    o["rs3.w32"] = _conv3_f32(sd[h + "resize_layers.3.weight"])
+    o["rs3.b"] = f32(sd[h + "resize_layers.3.bias"])
+    for i in range(4):
+        o[f"rn{i + 1}.w32"] = _conv3_f32(sd[f"{h}scratch.layer{i + 1}_rn.weight"])
+    for r in range(1, 5):
+        s = f"{h}scratch.refinenet{r}."
+        w = sd[s + "out_conv.weight"]
+        o[f"rf{r}.out.w32"] = _pad2_f32(w.reshape(w.shape[0], w.shape[1]))
+        o[f"rf{r}.out.b"] = f32(sd[s + "out_conv.bias"])
+        for u in (1, 2):
+            for c in (1, 2):
+                o[f"rf{r}.rcu{u}.c{c}.w32"] = _conv3_f32(sd[f"{s}resConfUnit{u}.conv{c}.weight"])
+                o[f"rf{r}.rcu{u}.c{c}.b"] = f32(sd[f"{s}resConfUnit{u}.conv{c}.bias"])
+    s = h + "scratch."
+    o["head.c1.w32"] = _conv3_f32(sd[s + "output_conv1.weight"])
+    o["head.c1.b"] = f32(sd[s + "output_conv1.bias"])
+    o["head.c2.w32"] = _conv3_f32(sd[s + "output_conv2.0.weight"])
+    o["head.c2.b"] = f32(sd[s + "output_conv2.0.bias"])
+    o["head.c3.w"] = f32(sd[s + "output_conv2.2.weight"])
+    o["head.c3.b"] = f32(sd[s + "output_conv2.2.bias"])
 
 
 INPUT_FORMATS = ("float32_nchw", "uint8_nhwc")

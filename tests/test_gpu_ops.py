@@ -654,6 +654,63 @@ def test_linear32_k_below_one_step(gpu):
     close(out, ref.float(), 2e-5, 2e-5, "linear32 K=16")
 
 
+@pytest.mark.parametrize("B,h,w,cin,cout,stride,relu_in,act,res", [
+    (2, 20, 22, 48, 64, 1, 0, 0, 0),     # layer1_rn: 48 input channels (ViT-S), K = 432 (tail)
+    (1, 37, 37, 64, 64, 1, 1, 1, 0),     # RCU conv1: ReLU on the operand and the output
+    (2, 19, 19, 64, 64, 1, 0, 0, 2),     # RCU conv2: + x + fusion skip
+    (1, 37, 37, 384, 384, 2, 0, 0, 0),   # resize_layers.3: stride 2
+    (1, 41, 53, 32, 32, 1, 0, 1, 0),     # output_conv2 shape (32 -> 32, ReLU)
+])
+def test_conv3x3_32(gpu, B, h, w, cin, cout, stride, relu_in, act, res):
+    """The exact-fp32 DPT head's conv (implicit im2col on the fp32 MFMA)
+    against a float64 torch conv2d: fp32 rounding only (2e-5)."""
+    x, wt, b = rn(B, cin, h, w), rn(cout, cin, 3, 3, scale=(9 * cin) ** -0.5), rn(cout, scale=0.1)
+    xin = F.relu(x.double()) if relu_in else x.double()
+    ref = F.conv2d(xin, wt.double(), b.double(), stride=stride, padding=1)
+    if act:
+        ref = F.relu(ref)
+    r0 = rn(*ref.shape) if res >= 1 else None
+    r1 = rn(*ref.shape) if res >= 2 else None
+    if r0 is not None:
+        ref = ref + r0.double()
+    if r1 is not None:
+        ref = ref + r1.double()
+    wp = pad_w32(wt.permute(0, 2, 3, 1).reshape(cout, 9 * cin)).to(gpu)
+    oh, ow = ref.shape[2], ref.shape[3]
+    out = torch.empty(B, oh, ow, cout, device=gpu)
+    keep = [nhwc(t).contiguous().to(gpu) for t in (r0, r1) if t is not None]
+    op("mde_op_conv3x3_32", ptr(nhwc(x).contiguous().to(gpu)), B, h, w, cin, ptr(wp), wp.shape[1], cout, stride,
+       relu_in, ptr(b.to(gpu)), act, ptr(keep[0]) if len(keep) > 0 else None, ptr(keep[1]) if len(keep) > 1 else None,
+       ptr(out), stream())
+    close(nchw(out), ref.float(), 2e-5, 2e-5, f"conv3x3_32 {h}x{w} {cin}->{cout} s{stride}")
+
+
+@pytest.mark.parametrize("s,cin,cout,B,h,w", [(4, 48, 48, 2, 7, 9), (2, 96, 96, 1, 37, 37), (4, 256, 256, 1, 5, 5)])
+def test_conv_transpose32(gpu, s, cin, cout, B, h, w):
+    """resize_layers 0 / 1 (ConvTranspose k = s) in fp32 against float64 torch."""
+    x = rn(B, cin, h, w)
+    wt, b = rn(cin, cout, s, s, scale=cin ** -0.5), rn(cout, scale=0.02)
+    ref = F.conv_transpose2d(x.double(), wt.double(), b.double(), stride=s)
+    wp = pad_w32(wt.permute(2, 3, 1, 0).reshape(s * s * cout, cin)).to(gpu)
+    out = torch.empty(B, h * s, w * s, cout, device=gpu)
+    op("mde_op_conv_transpose32", ptr(nhwc(x).contiguous().to(gpu)), B, h, w, cin, ptr(wp), wp.shape[1], cout, s,
+       ptr(b.to(gpu)), ptr(out), stream())
+    close(nchw(out), ref.float(), 2e-5, 2e-5, f"convT32 s{s}")
+
+
+@pytest.mark.parametrize("ih,iw,oh,ow,c", [(19, 19, 37, 37, 64), (148, 148, 296, 296, 64), (296, 296, 518, 518, 32),
+                                           (28, 37, 56, 74, 256), (5, 7, 1, 9, 16)])
+def test_resize32(gpu, ih, iw, oh, ow, c):
+    """fp32 bilinear align_corners against torch's fp32 F.interpolate (the
+    same index math: fp32 source coordinate, then the two-axis blend)."""
+    B = 2
+    x = rn(B, c, ih, iw)
+    ref = F.interpolate(x, size=(oh, ow), mode="bilinear", align_corners=True)
+    out = torch.empty(B, oh, ow, c, device=gpu)
+    op("mde_op_resize32", ptr(nhwc(x).contiguous().to(gpu)), B, ih, iw, c, oh, ow, ptr(out), stream())
+    close(nchw(out), ref, 2e-6, 2e-6, "resize32")
+
+
 def test_linear_residual32(gpu):
     m, n, k = 1370, 384, 1536
     a, w, b = rn(m, k), rn(n, k, scale=k ** -0.5), rn(n, scale=0.1)

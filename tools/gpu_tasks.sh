@@ -13,6 +13,7 @@
 #   profile:TAG:ARGS      tools/profile_round.sh (stats + FETCH/WRITE passes) -> OUT/prof_TAG/
 #   pmc:TAG:ARGS          tools/pmc_profile.sh on bench.py ARGS (SQ/TCC passes) -> OUT/pmc_TAG/
 #   kpmc:TAG:ARGS         tools/pmc_profile.sh on tools/bench_kernels.py ARGS    -> OUT/kpmc_TAG/
+#   trace:TAG:ARGS        rocprofv3 kernel + memory-copy trace of bench.py ARGS -> OUT/trace_TAG/
 #   kern:TAG:ARGS         tools/bench_kernels.py ARGS                 -> OUT/kern_TAG.log
 #   env:VAR=VAL           export VAR=VAL for the tasks that follow (e.g. env:MDE_ATTN_CFG=8)
 #   unenv:VAR             unset VAR
@@ -49,6 +50,10 @@ for t in "$@"; do
     pmc)
       bash tools/pmc_profile.sh "$O/pmc_$tag" -- python3 bench.py --steps 3 --warmup 1 --no-b1 --no-cpu-baseline \
         --profile-iters 1 "${args[@]}" || { log "pmc rc=$?"; exit 1; } ;;
+    trace)
+      timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$O/trace_$tag" -o tr -- \
+        python3 bench.py --no-b1 --no-cpu-baseline --profile-iters 1 "${args[@]}" > "$O/trace_$tag.log" 2>&1 \
+        || { log "trace rc=$?"; tail -20 "$O/trace_$tag.log"; exit 1; } ;;
     kpmc)
       bash tools/pmc_profile.sh "$O/kpmc_$tag" -- python3 tools/bench_kernels.py --iters 3 "${args[@]}" \
         || { log "kpmc rc=$?"; exit 1; } ;;
