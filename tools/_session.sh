@@ -1,8 +1,7 @@
 set -o pipefail
-O=gpurun_out/r5s3
+O=gpurun_out/r5s4
 mkdir -p $O
-bash tools/gpu_tasks.sh $O "tests:conv3x3_32 or conv_transpose32 or resize32 or fp32_precision or linear32 or attention32 or qkv32" \
-  bench:fp32:--precision,fp32,--batch,8,--no-cpu-baseline \
-  trace:pcie:--steps,10,--warmup,3 \
-  kern:a5:--batch,48,--iters,50,--only,attention,--attn-cfgs,8+4q2+8+4q2+8+4q2 \
-  pmc:def:
+bash tools/gpu_tasks.sh $O "tests:attention" \
+  bench:pk1:--no-b1,--no-cpu-baseline env:MDE_ATTN_PACK=0 bench:pk0:--no-b1,--no-cpu-baseline unenv:MDE_ATTN_PACK \
+  bench:pk1b:--no-b1,--no-cpu-baseline env:MDE_ATTN_PACK=0 bench:pk0b:--no-b1,--no-cpu-baseline unenv:MDE_ATTN_PACK \
+  kern:a6:--batch,48,--iters,50,--only,attention,--attn-cfgs,8+8p+8+8p+8+8p

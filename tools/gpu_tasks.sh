@@ -30,7 +30,7 @@ for t in "$@"; do
   case $name in
     tests)
       k=(); [ -n "$tag" ] && k=(-k "$tag")
-      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread "${k[@]}" \
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v -rP --timeout 120 --timeout-method thread "${k[@]}" \
         > "$O/tests.log" 2>&1 || { log "tests rc=$?"; tail -30 "$O/tests.log"; exit 1; } ;;
     smoke)
       timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.build(); g.smoke()" > "$O/smoke.log" 2>&1 \
