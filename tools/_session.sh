@@ -1,11 +1,7 @@
 set -o pipefail
-O=gpurun_out/r5s8
+O=gpurun_out/r5s9
 mkdir -p $O
-run() { echo "== $*" >> $O/ring.log; timeout -k 5 60 "$@" >> $O/ring.log 2>&1; }
-run ./build/rg_bk64 1370 3072 1024 50 && run ./build/rg_bk64_gm1 1370 3072 1024 50 && \
-run ./build/rg_128x64 1280 1536 1024 50 && run ./build/rg_128x64_g4 1280 1536 1024 50 && \
-bash tools/gpu_tasks.sh $O kern:t1370:--dim,1024,--heads,16,--batch,1,--tokens,1370,--only,N3072,--cold \
-  kern:t1280:--dim,1024,--heads,16,--batch,1,--tokens,1280,--only,N3072,--cold \
-  kern:t1024:--dim,1024,--heads,16,--batch,1,--tokens,1024,--only,N3072,--cold \
-  kern:t2048:--dim,1024,--heads,16,--batch,1,--tokens,2048,--only,N3072,--cold \
-  kern:f1024:--dim,1024,--heads,16,--batch,1,--tokens,1024,--only,fc1,--cold
+bash tools/gpu_tasks.sh $O "tests:l2pf or small_grid_variants or linear_splitk or fc2_splitk" \
+  kern:p0:--dim,1024,--heads,16,--batch,1,--only,N3072,--cold env:MDE_L2PF=1 kern:p1:--dim,1024,--heads,16,--batch,1,--only,N3072,--cold unenv:MDE_L2PF \
+  bench:l0:--encoder,vitl,--batch,1,--no-cpu-baseline,--no-pcie env:MDE_L2PF=1 bench:l1:--encoder,vitl,--batch,1,--no-cpu-baseline,--no-pcie unenv:MDE_L2PF \
+  bench:l0b:--encoder,vitl,--batch,1,--no-cpu-baseline,--no-pcie env:MDE_L2PF=1 bench:l1b:--encoder,vitl,--batch,1,--no-cpu-baseline,--no-pcie unenv:MDE_L2PF
