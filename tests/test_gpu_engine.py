@@ -376,7 +376,8 @@ def test_fp32_precision_engine_vs_golden_518(gpu, encoder):
     m = check(y, z["output_hf_f16"].astype(np.float32), 20.0, f"{name} exact-fp32 encoder vs HF golden", encoder,
               extra_abs=F16_Q)
     # against the f16-stored golden: the storage rounding (<= 2^-11 relative)
-    # is all that should remain -- the f16 head left 6.07e-4 (ViT-S) in round 4
+    # is all that should remain (measured 1.77e-4 / 1.72e-4 for ViT-S / ViT-L;
+    # the f16 head left 6.07e-4 at ViT-S in round 4)
     assert m["rel_mean"] <= 3e-4, m
 
 
@@ -393,7 +394,9 @@ def test_fp32_precision_engine_vs_oracle_98(gpu, encoder, B):
     ref = dav2_ref.forward(dav2_ref.to_torch(sd), cfg, x).numpy()
     y = run_engine(pack.pack_bytes(sd, cfg, 98, 98, precision="fp32"), x)
     m = check(y, ref, 20.0, f"{encoder} 98 B={B} exact-fp32 vs oracle", encoder)
-    assert m["rel_mean"] <= 2e-5 and m["max_abs"] <= 2e-3, m
+    # measured (MI355X, round 5): ViT-S rel_mean 6.1e-7 / max 3.9e-5 m, ViT-L
+    # 1.2e-6 / 4.1e-5 m -- fp32 rounding; the bars are ~5x that
+    assert m["rel_mean"] <= 5e-6 and m["max_abs"] <= 2e-4, m
 
 
 def test_fp32_precision_range_beyond_f16(gpu):
