@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define MDE_ABI_VERSION 7
+#define MDE_ABI_VERSION 8
 
 typedef enum {
   MDE_OK = 0,
@@ -102,7 +102,8 @@ const char* mde_last_error(void);
  * GEMM tiles (0 never, 1 auto, 2 always); "deep64" (0-1, 1) 4-deep ring for
  * small-grid 64^2 tiles; "w8small" (0-1, 1) 8-wave small-grid 128^2 tiles;
  * "conv_persist" (0-2, 1) persistent 64-channel RCU conv (1: 16 x 16 tiles,
- * 2: 8 x 16).  The environment variable of a switch is exactly
+ * 2: 8 x 16); "panel" (0-1, 0) A-stationary ping-pong GEMM for the K = 384
+ * qkv / fc1 at large batch.  The environment variable of a switch is exactly
  * MDE_ + its name upper-cased (MDE_DEEP64, MDE_W8SMALL, ...); a value that is
  * not an integer in range is reported on stderr and ignored.
  * Every setting computes the same depth map within the stated tolerance; the
@@ -188,6 +189,12 @@ int mde_op_linear_residual_f16(const void* a_f16, int lda, const void* w_f16, in
 int mde_op_linear_lnfold(const void* x_f16, const float* ln_partials, float eps, const void* wg_f16, int ldw,
                          const float* c1, const float* c2, int m, int n, int k, int act, void* out_f16, int ldo,
                          void* stream);
+/* mde_op_qkv with the LayerNorm folded in the same way (the DA-V2 engines' block qkv: norm1 ->
+ * qkv, reference depth_anything_v2/dinov2_layers/block.py attn(norm1(x))): x [batch*tokens][64 heads]
+ * raw f16 rows, ln_partials [heads*2][batch*tokens][2], wg = W * gamma, c1 / c2 as above. */
+int mde_op_qkv_lnfold(const void* x_f16, const float* ln_partials, float eps, const void* wg_f16, int ldw,
+                      const float* c1, const float* c2, int batch, int tokens, int heads, int tokens_pad,
+                      float q_scale, void* q_f16, void* k_f16, void* vt_f16, void* stream);
 /* q pre-multiplied by dh^-0.5 * log2(e) (scores in log2 units, as mde_op_qkv writes with
  * q_scale = 0.125 * log2(e)); k/q [B*H][tokens_pad][64], vt [B*H][64][tokens_pad] with key t
  * stored at column vt_pos(t) = t with bits 2 and 3 swapped, (t & ~12) | (t & 4) << 1 | (t & 8) >> 1

@@ -21,7 +21,7 @@ LIB = os.path.join(HERE, "libmde_hip.so")
 OBJDIR = os.path.join(ROOT, "build", "obj")
 ARCH = os.environ.get("MDE_OFFLOAD_ARCH", "gfx950")
 SOURCES = ["gemm.hip", "conv.hip", "attention.hip", "elementwise.hip", "engine.hip",
-           "depth_pro.hip", "depth_pro_ops.hip", "gemm256.hip", "vggt.hip", "vggt_ops.hip", "tuning.hip", "fp32.hip"]
+           "depth_pro.hip", "depth_pro_ops.hip", "gemm256.hip", "gemm_panel.hip", "vggt.hip", "vggt_ops.hip", "tuning.hip", "fp32.hip"]
 # attention / conv: no NaN inputs by construction (masked keys are -inf, never
 # NaN; activations finite); lets fmaxf / the ReLUs lower to a bare v_max
 # without canonicalising moves (v_pk_max_f16 x, x before every f16 ReLU)

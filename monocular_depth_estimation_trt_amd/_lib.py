@@ -108,6 +108,8 @@ PROTOTYPES = {
                                    c_void_p, c_int, c_void_p, c_void_p],
     "mde_op_linear_lnfold": [c_void_p, c_void_p, c_float, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
                              c_int, c_void_p, c_int, c_void_p],
+    "mde_op_qkv_lnfold": [c_void_p, c_void_p, c_float, c_void_p, c_int, c_void_p, c_void_p, c_int, c_int, c_int,
+                          c_int, c_float, c_void_p, c_void_p, c_void_p, c_void_p],
     "mde_op_attention_ws": [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_int, c_void_p,
                             c_size_t, c_void_p],
     "mde_op_attention_ws_bytes": [c_int, c_int, c_int],
@@ -245,7 +247,7 @@ def call(name: str, *args) -> None:
         raise MDEError(name, rc, last_error())
 
 
-TUNING = ("splitk", "lnfold", "conv_narrow", "upconv", "gemm256", "deep64", "w8small", "conv_persist")
+TUNING = ("splitk", "lnfold", "conv_narrow", "upconv", "gemm256", "deep64", "w8small", "conv_persist", "panel")
 
 
 def get_tuning(name: str) -> int:

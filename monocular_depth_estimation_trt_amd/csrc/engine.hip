@@ -1486,6 +1486,37 @@ int mde_op_linear_lnfold(const void* x, const float* ln_partials, float eps, con
   OP_RET(launch_gemm(g, (hipStream_t)st), "linear_lnfold");
 }
 
+int mde_op_qkv_lnfold(const void* x, const float* ln_partials, float eps, const void* wg, int ldw, const float* c1,
+                      const float* c2, int batch, int tokens, int heads, int tokens_pad, float qscale, void* q, void* k,
+                      void* vt, void* st) {
+  if (!x || !ln_partials || !wg || !c1 || !c2 || !q || !k || !vt) return fail(MDE_ERR_ARG, "null argument");
+  if (tokens_pad < tokens) return fail(MDE_ERR_ARG, "tokens_pad < tokens");
+  GemmParams g;
+  g.emode = E_QKV;
+  const int D = heads * 64;
+  g.A = (const h16*)x;
+  g.lda = D;
+  g.W = (const h16*)wg;
+  g.ldw = ldw;
+  g.M = batch * tokens;
+  g.N = 3 * D;
+  g.K = D;
+  g.bias = c2;
+  g.q = (h16*)q;
+  g.k = (h16*)k;
+  g.vt = (h16*)vt;
+  g.T = tokens;
+  g.Tpad = tokens_pad;
+  g.heads = heads;
+  g.qscale = qscale;
+  g.lnst_in = ln_partials;
+  g.lnc1 = c1;
+  g.lnst_ns = D / 32;
+  g.lnst_rows = g.M;
+  g.ln_eps = eps;
+  OP_RET(launch_gemm(g, (hipStream_t)st), "qkv_lnfold");
+}
+
 int mde_op_attention(const void* q, const void* k, const void* vt, void* o, int batch, int heads, int tokens,
                      int tokens_pad, int ldo, void* st) {
   if (!q || !k || !vt || !o) return fail(MDE_ERR_ARG, "null argument");

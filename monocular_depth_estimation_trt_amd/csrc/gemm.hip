@@ -220,6 +220,9 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
     kt0 = slice * per;
     nk = min(nk - kt0, per);  // >= 1: the launcher uses at most nk slices of ceil(nk / S) tiles
   }
+#ifdef MDE_EXP_NOLOOP
+  if (p.M > 0) nk = 0;
+#endif
 
   // conv K position (tap, c0) of this lane's chunk at K-tile kt0, advanced by
   // BK per step
@@ -241,6 +244,9 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
   f16x8 ru[UPC];
 
   auto issue = [&](int kt, int buf) {
+#ifdef MDE_EXP_NOLOAD
+    if (p.M > 0) return;
+#endif
     char* sbase = smem + buf * STAGE;
     const int k0 = (kt + kt0) * BK;
 #pragma unroll
@@ -314,6 +320,9 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
     for (int j = 0; j < TN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   auto mma_stage = [&](int cur) {
+#ifdef MDE_EXP_NOMFMA
+    if (p.M > 0) return;
+#endif
     const char* sA = smem + cur * STAGE;
     const char* sB = sA + BM * ROWB;
 #pragma unroll
@@ -376,23 +385,11 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
 #pragma unroll
         for (int g = 0; g < G; ++g) {
           const int r = wave * RPW + g * 16 + (lane & 15);
-          float s1 = 0.f;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) s1 += k < kp ? t[g][k].x : 0.f;
-          s1 += __shfl_xor(s1, 16);
-          s1 += __shfl_xor(s1, 32);
-          const float mean = s1 * invd;
-          float m2 = 0.f;
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {
-            const float d = t[g][k].x * (1.f / 32.f) - mean;
-            m2 += k < kp ? t[g][k].y + 32.f * d * d : 0.f;
-          }
-          m2 += __shfl_xor(m2, 16);
-          m2 += __shfl_xor(m2, 32);
+          float mean, var;
+          ln_merge_stats(t[g], kp, invd, mean, var);
           // only this wave's rows (RPW 8: lanes 8..15 hold the next wave's)
           if ((lane >> 4) == 0 && g * 16 + (lane & 15) < RPW)
-            *reinterpret_cast<float2*>(smem + SG * STAGE + r * 8) = make_float2(mean, m2 * invd);
+            *reinterpret_cast<float2*>(smem + SG * STAGE + r * 8) = make_float2(mean, var);
         }
       }
     }
@@ -429,6 +426,9 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
     }
   }
 
+#ifdef MDE_EXP_NOEPI
+  if (p.M > 0) return;
+#endif
   // ---- folded LayerNorm (GemmParams::lnst_in): A held the raw f16 residual
   // rows and W = W_ln * gamma; per row, mean and rstd from the producer's
   // 32-column partials (fp32), then acc := rstd * acc - rstd * mean * lnc1[n]
@@ -441,7 +441,7 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
       for (int i = 0; i < TM; ++i) {
         const float2 mv = *reinterpret_cast<const float2*>(smem + SG * STAGE + (wm * TM * 16 + i * 16 + (lane & 15)) * 8);
         const float mean = mv.x;
-        const float rstd = rsqrtf(mv.y + p.ln_eps);
+        const float rstd = rsqrtf(__fadd_rn(mv.y, p.ln_eps));
         const float nm = -rstd * mean;
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
@@ -710,6 +710,9 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
     // 32-column slice from the LDS-staged epilogue, the fold after the main loop;
     // a tile that falls back to the direct epilogue writes NaN partials)
     if (!lnst_valid(p)) return hipErrorInvalidValue;
+    if (panel_gemm_eligible(p)) return launch_panel_gemm(p, st);
+  } else if (panel_gemm_eligible(p)) {
+    return launch_panel_gemm(p, st);
   } else if (gemm256_eligible(p)) {
     return launch_gemm256(p, st);
   }

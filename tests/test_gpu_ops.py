@@ -69,7 +69,10 @@ def test_linear_residual(gpu, m, n, k):
                                    # inside tiles at every token alignment (T % 4 = 1, 3)
                                    (100, 37, 6), (3, 1371, 6),
                                    # D 1024, 75 x 12 tiles of 256^2 (>= 80 % of 4 rounds): gemm256 E_QKV
-                                   (14, 1370, 16)])
+                                   (14, 1370, 16),
+                                   # >= 64 panels of 256 rows: the panel kernel (gemm_panel.hip), V^T
+                                   # quads cut by image boundaries at T % 4 = 1 / 3
+                                   (480, 37, 6), (12, 1371, 6)])
 def test_qkv_layout(gpu, B, T, H):
     D = 64 * H
     Tp = -(-T // 64) * 64
@@ -92,6 +95,67 @@ def test_qkv_layout(gpu, B, T, H):
     pad = torch.ones(Tp, dtype=torch.bool, device=gpu)
     pad[perm] = False
     assert float(q[:, T:].abs().max()) == 0 and float(vt[:, :, pad].abs().max()) == 0, "pad must stay zero"
+
+
+@pytest.mark.parametrize("case", ["linear_gelu", "linear_none", "linear_relu_tail", "lnfold_gelu",
+                                  "qkv_1370", "qkv_37", "qkv_lnfold"])
+def test_panel_gemm_bit_exact(gpu, case):
+    """Switch "panel" (gemm_panel.hip: A-stationary 256-row panels, ping-pong
+    wave groups) against the 128^2 BK 32 kernel it replaces for K = 384 at
+    large M: the same MFMA k order and the same fp32 epilogue operations, so
+    every output must be equal bit for bit -- including the V^T third, whose
+    MFMAs run with the operands swapped, and M not a multiple of 256."""
+    from monocular_depth_estimation_trt_amd import _lib
+    k = 384
+    if case.startswith("linear") or case.startswith("lnfold"):
+        m = {"linear_gelu": 16384, "linear_none": 21920, "linear_relu_tail": 16397, "lnfold_gelu": 38360}[case]
+        n = 1536 if case != "linear_none" else 1152
+        act = {"linear_gelu": 2, "linear_none": 0, "linear_relu_tail": 1, "lnfold_gelu": 2}[case]
+        x = (rn(m, k) * 2 + 0.3).half().to(gpu)
+        w, b = rn(n, k, scale=k ** -0.5), rn(n, scale=0.1).to(gpu)
+        wp = pad_w(w).to(gpu)
+        part = ln_partials_ref(x.cpu()).float().to(gpu)
+        c1 = rn(n).to(gpu)
+        outs = []
+        for panel in (1, 0):
+            out = torch.full((m, n), float("nan"), dtype=torch.float16, device=gpu)
+            with _lib.tuning(panel=panel):
+                if case == "lnfold_gelu":
+                    op("mde_op_linear_lnfold", ptr(x), ptr(part), 1e-6, ptr(wp), wp.shape[1], ptr(c1), ptr(b), m, n,
+                       k, act, ptr(out), n, stream())
+                else:
+                    op("mde_op_linear", ptr(x), k, ptr(wp), wp.shape[1], m, n, k, ptr(b), act, ptr(out), n, stream())
+            outs.append(out)
+        assert torch.isfinite(outs[0]).all(), case
+        d = (outs[0].float() - outs[1].float()).abs()
+        assert torch.equal(outs[0], outs[1]), \
+            f"{case}: panel kernel differs from the 128^2 kernel ({int((d > 0).sum())} elements, max {float(d.max())})"
+        return
+    B, T, H = {"qkv_1370": (16, 1370, 6), "qkv_37": (480, 37, 6), "qkv_lnfold": (16, 1370, 6)}[case]
+    D = 64 * H
+    Tp = -(-T // 64) * 64
+    a = (rn(B * T, D) * 2 + 0.3).half().to(gpu)
+    w, b = rn(3 * D, D, scale=D ** -0.5), rn(3 * D, scale=0.1).to(gpu)
+    wp = pad_w(w).to(gpu)
+    part = ln_partials_ref(a.cpu()).float().to(gpu)
+    c1 = rn(3 * D).to(gpu)
+    res = []
+    for panel in (1, 0):
+        q = torch.zeros(B * H, Tp, 64, dtype=torch.float16, device=gpu)
+        kk = torch.zeros_like(q)
+        vt = torch.zeros(B * H, 64, Tp, dtype=torch.float16, device=gpu)
+        with _lib.tuning(panel=panel):
+            if case == "qkv_lnfold":
+                op("mde_op_qkv_lnfold", ptr(a), ptr(part), 1e-6, ptr(wp), wp.shape[1], ptr(c1), ptr(b), B, T, H, Tp,
+                   0.125, ptr(q), ptr(kk), ptr(vt), stream())
+            else:
+                op("mde_op_qkv", ptr(a), ptr(wp), wp.shape[1], ptr(b), B, T, H, Tp, 0.125, ptr(q), ptr(kk), ptr(vt),
+                   stream())
+        res.append((q, kk, vt))
+    for name, x0, x1 in zip("q k vt".split(), res[0], res[1]):
+        d = (x0.float() - x1.float()).abs()
+        assert torch.equal(x0, x1), \
+            f"{case}: panel kernel {name} differs from the 128^2 kernel ({int((d > 0).sum())} elements, max {float(d.max())})"
 
 
 LOG2E = 1.4426950408889634
