@@ -60,21 +60,22 @@ MDE_DEV f32x2 gelu_erf2(f32x2 x) {
 // explicitly (no contraction), so the GEMM kernels that fold LN (gemm.hip,
 // gemm_panel.hip) compute bit-identical statistics whatever their code around.
 MDE_DEV void ln_merge_stats(const float2 (&t)[8], int kp, float invd, float& mean, float& var) {
+#pragma clang fp contract(off)
   float s1 = 0.f;
 #pragma unroll
-  for (int k = 0; k < 8; ++k) s1 = __fadd_rn(s1, k < kp ? t[k].x : 0.f);
-  s1 = __fadd_rn(s1, __shfl_xor(s1, 16));
-  s1 = __fadd_rn(s1, __shfl_xor(s1, 32));
-  mean = __fmul_rn(s1, invd);
+  for (int k = 0; k < 8; ++k) s1 = s1 + (k < kp ? t[k].x : 0.f);
+  s1 = s1 + __shfl_xor(s1, 16);
+  s1 = s1 + __shfl_xor(s1, 32);
+  mean = s1 * invd;
   float m2 = 0.f;
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const float d = __fsub_rn(__fmul_rn(t[k].x, 1.f / 32.f), mean);
-    m2 = __fadd_rn(m2, k < kp ? __fadd_rn(t[k].y, __fmul_rn(__fmul_rn(32.f, d), d)) : 0.f);
+    const float d = t[k].x * (1.f / 32.f) - mean;
+    m2 = m2 + (k < kp ? t[k].y + (32.f * d) * d : 0.f);
   }
-  m2 = __fadd_rn(m2, __shfl_xor(m2, 16));
-  m2 = __fadd_rn(m2, __shfl_xor(m2, 32));
-  var = __fmul_rn(m2, invd);
+  m2 = m2 + __shfl_xor(m2, 16);
+  m2 = m2 + __shfl_xor(m2, 32);
+  var = m2 * invd;
 }
 
 // PyTorch upsample_bilinear2d(align_corners=True) source index and weights

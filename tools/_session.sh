@@ -1,5 +1,6 @@
 set -o pipefail
-O=gpurun_out/r5x9
+O=gpurun_out/r5x17
 mkdir -p $O
-K=--batch,48,--iters,20,--only,K384
-bash tools/gpu_tasks.sh $O kern:pon:$K env:MDE_PANEL=0 kern:poff:$K unenv:MDE_PANEL "tests:panel or qkv_layout or test_linear"
+A=--no-b1,--no-cpu-baseline,--no-pcie
+bash tools/gpu_tasks.sh $O env:MDE_PANEL=1 bench:pon:$A unenv:MDE_PANEL bench:poff:$A env:MDE_PANEL=1 bench:pon2:$A \
+  "tests:engine_518_bench or replays or graph or lnfold or golden_518"

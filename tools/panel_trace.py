@@ -1,0 +1,62 @@
+"""Per-segment timing of the panel GEMM (gemm_panel.hip built with -DPX_TRACE):
+runs one fc1-shaped launch (ViT-S B=48: M 65760, N 1536, K 384, GELU) through
+the C ABI with the switch on, reads the s_memtime stamps of blocks 0-7 and
+prints, per group and segment kind, the work time and the barrier wait.
+
+    python tools/panel_trace.py LIB [--act 2] [--n 1536]
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("lib")
+    ap.add_argument("--act", type=int, default=2)
+    ap.add_argument("--n", type=int, default=1536)
+    ap.add_argument("--m", type=int, default=65760)
+    a = ap.parse_args()
+    import torch
+    from gpu_util import pad_w, ptr, stream
+    from monocular_depth_estimation_trt_amd import _lib
+    _lib.use_library(a.lib)
+    L = _lib.lib()
+    _lib.set_tuning("panel", 1)
+    dev = torch.device("cuda:0")
+    m, n, k = a.m, a.n, 384
+    x = torch.randn(m, k, device=dev).half()
+    wp = pad_w(torch.randn(n, k) * k ** -0.5).to(dev)
+    b = torch.randn(n, device=dev) * 0.1
+    out = torch.empty(m, n, dtype=torch.float16, device=dev)
+    for _ in range(3):
+        L.mde_op_linear(ptr(x), k, ptr(wp), wp.shape[1], m, n, k, ptr(b), a.act, ptr(out), n, stream())
+    torch.cuda.synchronize()
+    buf = np.zeros((8, 8, 96, 2), dtype=np.uint64)
+    fn = getattr(L, "mde_debug_panel_trace")
+    fn.argtypes = [C.c_void_p]
+    assert fn(buf.ctypes.data) == 0
+    t = buf.astype(np.int64)
+    nseg = int((t[0, 0, :, 0] > 0).sum())
+    print(f"units recorded per wave: {nseg}")
+    rows = []
+    for blk in range(8):
+        st, en = t[blk, :, :, 0], t[blk, :, :, 1]
+        for u in range(1, nseg - 1):
+            length = st[:, u + 1].max() - st[:, u].max()  # barrier to barrier
+            work = (en[:, u] - st[:, u]).mean()            # after barrier -> before the end-of-unit wait
+            tail = (st[:, u + 1] - en[:, u]).mean()        # wait + barrier
+            rows.append((length, work, tail))
+    r = np.array(rows, dtype=np.float64)
+    print(f"unit: length {r[:, 0].mean():8.0f}  work {r[:, 1].mean():8.0f}  wait+barrier {r[:, 2].mean():8.0f} (s_memtime ticks, n={len(r)})")
+
+
+if __name__ == "__main__":
+    main()
