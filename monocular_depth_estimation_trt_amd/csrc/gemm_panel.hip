@@ -54,31 +54,35 @@ constexpr int PSLOTS = 2;            // W ring depth
 constexpr int PNMAX = 1536;          // widest N (bias / lnc1 table)
 constexpr int PTAB = PSLOTS * PCHB;  // bias / lnc1 table offset
 constexpr int PLDS = PTAB + 2 * PNMAX * 4;  // 108 KB
+#ifndef PEPI_STRIDE
+#define PEPI_STRIDE 1  // k-substeps between the epilogue's block pairs
+#endif
+#ifndef PEPI_OFF1
+#define PEPI_OFF1 6    // first epilogue substep of waves 4-7 (waves 0-3: 0)
+#endif
 
-// One wave's share of a W chunk: 6 LDS-DMAs (global_load_lds_dwordx4, 64-bit
-// vaddr form) -- rows lane >> 3 of its 8-row slice, row segment ks of 128 B
-// from base + off + 128 ks into the LDS image at lds + 8192 ks.  Issued from
-// inline asm on purpose: a compiler-visible LDS-DMA counts as a pending LGKM
-// event in the compiler's wait insertion, which then turns every counted
-// lgkmcnt of the MFMA stream into lgkmcnt(0) (each substep stalled on the
-// fragment reads just issued for the next).  The 64-bit lane address is
-// formed inside the block (nothing loop-invariant for the compiler to keep
-// live) and advanced after each issue (the vaddr64 form reads it at issue:
-// tools/dma_war_probe.hip); m0 is restored.
-#define PGLDS_SEG(MOFF)                                                                    \
-  "s_add_u32 m0, %[l], " MOFF "\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[a], off\n\t" \
-  "v_lshl_add_u64 %[a], %[a], 0, %[st]\n\t"
-MDE_DEV void pglds_chunk(const void* base, unsigned off, unsigned lds) {
+// One wave's share of a W chunk: 6 LDS-DMAs (global_load_lds_dwordx4, SGPR
+// base + 32-bit VGPR offset form) -- rows lane >> 3 of its 8-row slice, row
+// segment ks of 128 B from base + 128 ks + off into the LDS image at
+// lds + 8192 ks.  Issued from inline asm on purpose: a compiler-visible
+// LDS-DMA counts as a pending LGKM event in the compiler's wait insertion,
+// which then turns every counted lgkmcnt of the MFMA stream into lgkmcnt(0)
+// (each substep stalled on the fragment reads just issued for the next).
+// The six segment bases are wave-uniform SGPR pairs and the lane offset one
+// VGPR that is never written here (no address register reuse; the form is
+// covered by tools/dma_war_probe.hip); m0 is restored.
+#define PGLDS_SEG(B, MOFF) \
+  "s_add_u32 m0, %[l], " MOFF "\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %[off], %[" B "]\n\t"
+MDE_DEV void pglds_chunk(const char* base, unsigned off, unsigned lds) {
   unsigned keep;
-  unsigned long long a;
   asm volatile(
       "s_mov_b32 %[keep], m0\n\t"
-      "v_lshl_add_u64 %[a], %[off], 0, %[b]\n\t"
-      PGLDS_SEG("0x0") PGLDS_SEG("0x2000") PGLDS_SEG("0x4000")
-      PGLDS_SEG("0x6000") PGLDS_SEG("0x8000") PGLDS_SEG("0xa000")
+      PGLDS_SEG("b0", "0x0") PGLDS_SEG("b1", "0x2000") PGLDS_SEG("b2", "0x4000")
+      PGLDS_SEG("b3", "0x6000") PGLDS_SEG("b4", "0x8000") PGLDS_SEG("b5", "0xa000")
       "s_mov_b32 m0, %[keep]"
-      : [keep] "=&s"(keep), [a] "=&v"(a)
-      : [off] "v"((unsigned long long)off), [b] "s"((unsigned long long)base), [l] "s"(lds), [st] "s"(128ull)
+      : [keep] "=&s"(keep)
+      : [off] "v"(off), [b0] "s"(base), [b1] "s"(base + 128), [b2] "s"(base + 256), [b3] "s"(base + 384),
+        [b4] "s"(base + 512), [b5] "s"(base + 640), [l] "s"(lds)
       : "memory");
 }
 #undef PGLDS_SEG
@@ -104,7 +108,7 @@ __device__ __attribute__((aligned(16))) f16x4 g_psink[64];
 #ifdef PX_TRACE
 // timing build only (tools/panel_trace.py): per (block < 8, wave, unit <
 // 96) the s_memtime after the unit's barrier and before its end-of-unit wait
-__device__ unsigned long long g_ptrace[8][8][96][2];
+__device__ unsigned long long g_ptrace[8][8][96][3];
 #define PTRACE(SG, K)                                                     \
   if (blockIdx.x < 8 && (SG) >= 0 && (SG) < 96) {                         \
     const unsigned long long tt = __builtin_amdgcn_s_memtime();           \
@@ -142,7 +146,7 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
   const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)smem) + wave * 1024;
   auto issue = [&](int rel) __attribute__((always_inline)) {  // unit u0 + rel -> slot rel & 1
     const int c = (u0 + rel) % nch;
-    pglds_chunk(reinterpret_cast<const f16*>(p.W) + (size_t)(c * PBN + 8 * wave) * p.ldw, woff,
+    pglds_chunk(reinterpret_cast<const char*>(p.W) + (size_t)(c * PBN + 8 * wave) * p.ldw * 2, woff,
                 lds0 + (rel & 1) * PCHB);
   };
 
@@ -290,8 +294,9 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
   // hoisting all 48 fragment reads (192 VGPRs) and keeps each epilogue block
   // beside its substep's 8 MFMAs.
   const int cx = (hq ^ (lane & 7)) << 4;  // physical chunk of logical chunk hq in rows r (r & 7 = lane & 7)
-  auto unit = [&](int j, f32x4(&accC)[2][4], const f32x4(&accP)[2][4], bool epi, int ppnl, int pc,
+  auto unit = [&](auto off_tag, int j, f32x4(&accC)[2][4], const f32x4(&accP)[2][4], bool epi, int ppnl, int pc,
                   const float (&pmean)[2], const float (&prstd)[2]) __attribute__((always_inline)) {
+    constexpr int OFF = decltype(off_tag)::value;
     const char* sw = smem + (j & 1) * PCHB + l15 * 128;
 #pragma unroll
     for (int ib = 0; ib < 2; ++ib)
@@ -307,67 +312,80 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
 #pragma unroll
     for (int s = 0; s < PKS; ++s) {
       if (s + 1 < PKS) rd(s + 1, wf[(s + 1) & 1]);
+      // the epilogue's 4 block pairs run in substeps OFF, OFF + E, .. OFF + 3E
+      constexpr int E = PEPI_STRIDE;
+      const bool ep = s >= OFF && ((s - OFF) % E) == 0 && (s - OFF) / E < 4;
+      const int q = (s - OFF) / E;
       ColB cb[2];
-      if (s < 4) cb[0] = col_read(pc, (2 * s) & 3), cb[1] = col_read(pc, (2 * s + 1) & 3);
+      if (ep) cb[0] = col_read(pc, (2 * q) & 3), cb[1] = col_read(pc, (2 * q + 1) & 3);
 #pragma unroll
       for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
         for (int jb = 0; jb < 4; ++jb) accC[ib][jb] = mfma16x16x32(wf[s & 1][jb], af[ib][s], accC[ib][jb]);
       // blocks 2s, 2s + 1 of the previous unit in substeps 0 .. 3: its stores
       // are then at least 8 substeps old at the end-of-unit wait
-      if (s < 4) epi_pair(2 * s, ppnl, pc, accP, pmean, prstd, cb, epi);
+      if (ep) epi_pair(2 * q, ppnl, pc, accP, pmean, prstd, cb, epi);
       __builtin_amdgcn_sched_barrier(0);
     }
   };
 
-  f32x4 acc0[2][4], acc1[2][4];  // this unit's / the previous unit's accumulators
-#pragma unroll
-  for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-    for (int jb = 0; jb < 4; ++jb) acc1[ib][jb] = f32x4{0.f, 0.f, 0.f, 0.f};
-  float lmean[2] = {0.f, 0.f}, lrstd[2] = {1.f, 1.f};  // stats of the unit whose epilogue runs next
-  int ppnl = 0, pc = 0;                                 // that unit's panel and chunk
-
-  // ---- prologue: chunk 0 in flight, the first panel loaded ----
+  // ---- prologue: chunk 0 in flight ----
   issue(0);
-  // ---- units; outer loop: one run of units per A panel (af loop-invariant inside)
-  int j = 0;
-  while (j < nu) {
-    const int pnl = (u0 + j) / nch;
-    const int jend = min(nu, (pnl + 1) * nch - u0);
-    load_panel(pnl);
-    float nmean[2] = {0.f, 0.f}, nrstd[2] = {1.f, 1.f};
-    if constexpr (FOLD) panel_stats(pnl, nmean, nrstd);
-    pwait_vm0();  // A and chunk j landed (once per panel)
-    if (j == 0) {
-      lmean[0] = nmean[0], lmean[1] = nmean[1];
-      lrstd[0] = nrstd[0], lrstd[1] = nrstd[1];
+  // ---- the unit loop, one copy per epilogue placement: the two waves of a
+  // SIMD (w, w + 4) run their epilogue VALU in different k-substeps, so one's
+  // VALU-heavy substeps meet the other's MFMA-only ones (the same substeps
+  // for both left the SIMD alternately VALU- and MFMA-bound and one of the
+  // pair idling at the unit barrier).  The branch sits outside the loop: a
+  // per-unit branch between two unit bodies merged both accumulator sets at
+  // every join and spilled.  Both copies run the same barrier sequence.
+  auto run = [&](auto off_tag) __attribute__((always_inline)) {
+    f32x4 acc0[2][4], acc1[2][4];  // this unit's / the previous unit's accumulators
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+      for (int jb = 0; jb < 4; ++jb) acc1[ib][jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float lmean[2] = {0.f, 0.f}, lrstd[2] = {1.f, 1.f};  // this panel's LN stats
+    int ppnl = 0, pc = 0;                                 // panel and chunk of the unit whose epilogue runs next
+    // outer loop: one run of units per A panel (af loop-invariant inside)
+    auto epi_all = [&]() __attribute__((always_inline)) {  // a unit's whole epilogue, standalone
+#pragma unroll
+      for (int b = 0; b < 8; ++b)
+        epi_block(b >> 2, b & 3, ppnl, pc, acc1[b >> 2][b & 3], lmean[b >> 2], lrstd[b >> 2], col_read(pc, b & 3),
+                  true);
+    };
+    int j = 0;
+    while (j < nu) {
+      const int pnl = (u0 + j) / nch;
+      const int jend = min(nu, (pnl + 1) * nch - u0);
+      // the previous panel's last epilogue runs here, on its own (once per
+      // panel switch): the stats registers then hold one panel at a time
+      if (j > 0) epi_all();
+      load_panel(pnl);
+      if constexpr (FOLD) panel_stats(pnl, lmean, lrstd);
+      pwait_vm0();  // A and chunk j landed (once per panel)
+      for (int j0 = j; j < jend; ++j) {
+        pbarrier();  // chunk j visible to all waves; slot (j + 1) & 1 (unit j - 1) fully read
+        PTRACE(j, 0)
+        if (j + 1 < nu) issue(j + 1);
+        // fixed accumulator roles and a copy per unit (32 moves per 96
+        // MFMAs): alternating the two sets by unit parity left both live
+        // across a branch and spilled
+        unit(off_tag, j, acc0, acc1, j > j0, pnl, pc, lmean, lrstd);
+#pragma unroll
+        for (int ib = 0; ib < 2; ++ib)
+#pragma unroll
+          for (int jb = 0; jb < 4; ++jb) acc1[ib][jb] = acc0[ib][jb];
+        ppnl = pnl;
+        pc = (u0 + j) - pnl * nch;
+        PTRACE(j, 1)
+        pwait_vm0();  // chunk j + 1 landed; this unit's stores done
+        PTRACE(j, 2)
+      }
     }
-    for (; j < jend; ++j) {
-      pbarrier();  // chunk j visible to all waves; slot (j + 1) & 1 (unit j - 1) fully read
-      PTRACE(j, 0)
-      if (j + 1 < nu) issue(j + 1);
-      // unit j - 1's epilogue runs with its own panel's stats; this panel's
-      // take over after it
-      // (fixed roles, a copy per unit: 32 moves per 96 MFMAs -- alternating
-      // the two sets by unit parity left both live across a branch and spilled)
-      unit(j, acc0, acc1, j > 0, ppnl, pc, lmean, lrstd);
-#pragma unroll
-      for (int ib = 0; ib < 2; ++ib)
-#pragma unroll
-        for (int jb = 0; jb < 4; ++jb) acc1[ib][jb] = acc0[ib][jb];
-      lmean[0] = nmean[0], lmean[1] = nmean[1];
-      lrstd[0] = nrstd[0], lrstd[1] = nrstd[1];
-      ppnl = pnl;
-      pc = (u0 + j) - pnl * nch;
-      PTRACE(j, 1)
-      pwait_vm0();  // chunk j + 1 landed; this unit's stores (>= 4 substeps old) done
-    }
-  }
-  // the last unit's epilogue
-#pragma unroll
-  for (int b = 0; b < 8; ++b)
-    epi_block(b >> 2, b & 3, ppnl, pc, acc1[b >> 2][b & 3], lmean[b >> 2], lrstd[b >> 2], col_read(pc, b & 3), true);
+    epi_all();  // the last unit's epilogue
+  };
+  if (wave < 4) run(std::integral_constant<int, 0>{});
+  else run(std::integral_constant<int, PEPI_OFF1>{});
 }
 
 int cu_count() {

@@ -39,7 +39,7 @@ def main():
     for _ in range(3):
         L.mde_op_linear(ptr(x), k, ptr(wp), wp.shape[1], m, n, k, ptr(b), a.act, ptr(out), n, stream())
     torch.cuda.synchronize()
-    buf = np.zeros((8, 8, 96, 2), dtype=np.uint64)
+    buf = np.zeros((8, 8, 96, 3), dtype=np.uint64)
     fn = getattr(L, "mde_debug_panel_trace")
     fn.argtypes = [C.c_void_p]
     assert fn(buf.ctypes.data) == 0
@@ -48,15 +48,17 @@ def main():
     print(f"units recorded per wave: {nseg}")
     rows = []
     for blk in range(8):
-        st, en = t[blk, :, :, 0], t[blk, :, :, 1]
+        st, en, wt = t[blk, :, :, 0], t[blk, :, :, 1], t[blk, :, :, 2]
         for u in range(1, nseg - 1):
             length = st[:, u + 1].max() - st[:, u].max()  # barrier to barrier
             work = (en[:, u] - st[:, u]).mean()            # after barrier -> before the end-of-unit wait
-            tail = (st[:, u + 1] - en[:, u]).mean()        # wait + barrier
-            rows.append((length, work, tail))
+            wait = (wt[:, u] - en[:, u]).mean()            # the vmcnt(0)
+            skew = (st[:, u + 1] - wt[:, u]).mean()        # waiting at the barrier
+            spread = (en[:, u] - st[:, u]).max() - (en[:, u] - st[:, u]).min()
+            rows.append((length, work, wait, skew, spread))
     r = np.array(rows, dtype=np.float64)
-    print(f"unit: length {r[:, 0].mean():8.0f}  work {r[:, 1].mean():8.0f}  wait+barrier {r[:, 2].mean():8.0f} (s_memtime ticks, n={len(r)})")
-
+    print(f"unit (s_memtime ticks, n={len(r)}): length {r[:, 0].mean():7.0f}  work {r[:, 1].mean():7.0f}  "
+          f"vmcnt wait {r[:, 2].mean():7.0f}  barrier {r[:, 3].mean():7.0f}  work spread over waves {r[:, 4].mean():7.0f}")
 
 if __name__ == "__main__":
     main()
