@@ -1,5 +1,5 @@
-// Short-K token-major GEMM at large batch (the ViT-S fc1: K = 384, GELU,
-// LayerNorm folded) for gfx950: A-stationary row panels, W chunks streamed
+// Short-K token-major GEMMs at large batch (the ViT-S fc1 and qkv: K = 384,
+// GELU / q-k-V^T head split, LayerNorm folded) for gfx950: A-stationary row panels, W chunks streamed
 // through LDS, each unit's MFMAs interleaved with the previous unit's
 // epilogue in the same wave.
 //
@@ -32,7 +32,8 @@
 //  * the workgroups are persistent: each takes a contiguous range of the
 //    (panel, chunk) units, so a panel's A is loaded once or twice per CU.
 //
-// Reference op covered: a12 fc1 + GELU (a10 LayerNorm folded).
+// Reference ops covered: a9 qkv, a12 fc1 + GELU (the a8 / a10
+// LayerNorms folded).
 #include <cstdlib>
 #include <type_traits>
 
@@ -118,7 +119,7 @@ __device__ unsigned long long g_ptrace[8][8][96][3];
 #define PTRACE(SG, K)
 #endif
 
-template <int ACT, bool FOLD>
+template <int EM, int ACT, bool FOLD>
 __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int nch, int npan) {
   __shared__ __attribute__((aligned(16))) char smem[PLDS];
   float* tab_b = reinterpret_cast<float*>(smem + PTAB);
@@ -201,6 +202,44 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
     r.c = FOLD ? *reinterpret_cast<const float4*>(tab_c + n) : float4{0.f, 0.f, 0.f, 0.f};
     return r;
   };
+  // the 4 outputs of block (ib, jb) of unit (pnl, c), one rounding to f16;
+  // rows >= M and the dummy epilogue of a run's first unit go to the sink.
+  // E_STORE: one 8-B store at (m, n .. n+3).  E_QKV (chunk c = head c % heads
+  // of q, k or v): q (scaled) / k rows [b*heads + h][t][64] take the 8 B at
+  // dh .. dh+3; V^T [b*heads + h][64][Tpad] takes 4 scalar stores at key
+  // position vt_pos(t) of rows dh .. dh+3
+  auto store4 = [&](int ib, int jb, int pnl, int c, float y0, float y1, float y2, float y3, bool live)
+                    __attribute__((always_inline)) {
+    const int m = row_of(pnl, ib);
+    const bool ok = live && m < p.M;
+    if constexpr (EM == E_STORE) {
+      const f16x4 h = {(f16)y0, (f16)y1, (f16)y2, (f16)y3};
+      const int n = c * PBN + jb * 16 + hq * 4;
+      f16x4* dst = ok ? reinterpret_cast<f16x4*>(reinterpret_cast<f16*>(p.out16) + (size_t)m * p.ldo + n) : g_psink + lane;
+      *dst = h;
+    } else {
+      const int which = c / p.heads, hh = c - which * p.heads;
+      const int mm = ok ? m : 0;
+      const int b = mm / p.T, t = mm - b * p.T;
+      const int dh = jb * 16 + hq * 4;
+      if (which < 2) {
+        const float sc = which == 0 ? p.qscale : 1.f;
+        const f16x4 h = {(f16)(y0 * sc), (f16)(y1 * sc), (f16)(y2 * sc), (f16)(y3 * sc)};
+        f16* base = which == 0 ? reinterpret_cast<f16*>(p.q) : reinterpret_cast<f16*>(p.k);
+        f16x4* dst = ok ? reinterpret_cast<f16x4*>(base + ((size_t)(b * p.heads + hh) * p.Tpad + t) * 64 + dh)
+                        : g_psink + lane;
+        *dst = h;
+      } else {
+        f16* row = reinterpret_cast<f16*>(p.vt) + ((size_t)(b * p.heads + hh) * 64 + dh) * p.Tpad + vt_pos(t);
+        f16* sink = reinterpret_cast<f16*>(g_psink + lane);
+        const size_t tp = p.Tpad;
+        *(ok ? row : sink) = (f16)y0;
+        *(ok ? row + tp : sink) = (f16)y1;
+        *(ok ? row + 2 * tp : sink) = (f16)y2;
+        *(ok ? row + 3 * tp : sink) = (f16)y3;
+      }
+    }
+  };
   auto epi_block = [&](int ib, int jb, int pnl, int c, const f32x4& a, float mean, float rstd, const ColB& cb,
                        bool live) __attribute__((always_inline)) {
     f32x4 v = a;
@@ -219,12 +258,7 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
       const f32x2 lo = gelu_erf2(f32x2{v[0], v[1]}), hi = gelu_erf2(f32x2{v[2], v[3]});
       v = f32x4{lo[0], lo[1], hi[0], hi[1]};
     }
-    const f16x4 h = {(f16)v[0], (f16)v[1], (f16)v[2], (f16)v[3]};
-    const int m = row_of(pnl, ib);
-    const int n = c * PBN + jb * 16 + hq * 4;
-    f16x4* dst = (live && m < p.M) ? reinterpret_cast<f16x4*>(reinterpret_cast<f16*>(p.out16) + (size_t)m * p.ldo + n)
-                                   : g_psink + lane;
-    *dst = h;
+    store4(ib, jb, pnl, c, v[0], v[1], v[2], v[3], live);
   };
   // two blocks (2 x 4 values) in lockstep: each step of gelu_erf2 for all
   // four value pairs before the next (the same operations per value, so
@@ -278,12 +312,7 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int b = b0 + e, ib = b >> 2, jb = b & 3;
-      const f16x4 h = {(f16)y[2 * e][0], (f16)y[2 * e][1], (f16)y[2 * e + 1][0], (f16)y[2 * e + 1][1]};
-      const int m = row_of(pnl, ib);
-      const int n = c * PBN + jb * 16 + hq * 4;
-      f16x4* dst = (live && m < p.M) ? reinterpret_cast<f16x4*>(reinterpret_cast<f16*>(p.out16) + (size_t)m * p.ldo + n)
-                                     : g_psink + lane;
-      *dst = h;
+      store4(ib, jb, pnl, c, y[2 * e][0], y[2 * e][1], y[2 * e + 1][0], y[2 * e + 1][1], live);
     }
   };
 
@@ -410,14 +439,18 @@ extern "C" int mde_debug_panel_trace(unsigned long long* host) {
 
 bool panel_gemm_eligible(const GemmParams& p) {
   if (!knob(KNOB_PANEL)) return false;
-  if (p.amode != A_DENSE || p.emode != E_STORE || p.K != PK || p.a_tok != 0 || p.lnst_out || p.splitk > 1)
-    return false;
+  if (p.amode != A_DENSE || p.K != PK || p.a_tok != 0 || p.lnst_out || p.splitk > 1) return false;
   if (p.N % PBN || p.N > PNMAX || (p.lda & 7) || p.lda < PK || p.ldw < PK || (p.ldw & 63)) return false;
   if (p.lnst_in && (!p.lnc1 || p.lnst_ns != PK / 32 || p.lnst_rows != p.M)) return false;
   // whole CUs of work: at least 64 panels (B >= 12 ViT-S images)
   if ((p.M + PBM - 1) / PBM < 64) return false;
-  return p.out16 && !p.res0 && !p.res1 && !(p.ldo & 3) && !((uintptr_t)p.out16 & 7) && p.ldo >= p.N &&
-         (p.act == ACT_NONE || p.act == ACT_RELU || p.act == ACT_GELU);
+  if (p.emode == E_STORE)
+    return p.out16 && !p.res0 && !p.res1 && !(p.ldo & 3) && !((uintptr_t)p.out16 & 7) && p.ldo >= p.N &&
+           (p.act == ACT_NONE || p.act == ACT_RELU || p.act == ACT_GELU);
+  if (p.emode == E_QKV)
+    return p.heads > 0 && p.heads * 64 * 3 == p.N && p.T > 0 && p.Tpad >= p.T && p.q && p.k && p.vt &&
+           !((uintptr_t)p.q & 7) && !((uintptr_t)p.k & 7) && p.act == ACT_NONE;
+  return false;
 }
 
 hipError_t launch_panel_gemm(const GemmParams& p, hipStream_t st) {
@@ -425,14 +458,17 @@ hipError_t launch_panel_gemm(const GemmParams& p, hipStream_t st) {
   const int U = nch * npan;
   const int G = U < cu_count() ? U : cu_count();
   const dim3 g(G), b(512);
-  if (p.lnst_in) {
-    if (p.act == ACT_GELU) hipLaunchKernelGGL((panel_gemm_kernel<ACT_GELU, true>), g, b, 0, st, p, nch, npan);
-    else if (p.act == ACT_RELU) hipLaunchKernelGGL((panel_gemm_kernel<ACT_RELU, true>), g, b, 0, st, p, nch, npan);
-    else hipLaunchKernelGGL((panel_gemm_kernel<ACT_NONE, true>), g, b, 0, st, p, nch, npan);
+  if (p.emode == E_QKV) {
+    if (p.lnst_in) hipLaunchKernelGGL((panel_gemm_kernel<E_QKV, ACT_NONE, true>), g, b, 0, st, p, nch, npan);
+    else hipLaunchKernelGGL((panel_gemm_kernel<E_QKV, ACT_NONE, false>), g, b, 0, st, p, nch, npan);
+  } else if (p.lnst_in) {
+    if (p.act == ACT_GELU) hipLaunchKernelGGL((panel_gemm_kernel<E_STORE, ACT_GELU, true>), g, b, 0, st, p, nch, npan);
+    else if (p.act == ACT_RELU) hipLaunchKernelGGL((panel_gemm_kernel<E_STORE, ACT_RELU, true>), g, b, 0, st, p, nch, npan);
+    else hipLaunchKernelGGL((panel_gemm_kernel<E_STORE, ACT_NONE, true>), g, b, 0, st, p, nch, npan);
   } else {
-    if (p.act == ACT_GELU) hipLaunchKernelGGL((panel_gemm_kernel<ACT_GELU, false>), g, b, 0, st, p, nch, npan);
-    else if (p.act == ACT_RELU) hipLaunchKernelGGL((panel_gemm_kernel<ACT_RELU, false>), g, b, 0, st, p, nch, npan);
-    else hipLaunchKernelGGL((panel_gemm_kernel<ACT_NONE, false>), g, b, 0, st, p, nch, npan);
+    if (p.act == ACT_GELU) hipLaunchKernelGGL((panel_gemm_kernel<E_STORE, ACT_GELU, false>), g, b, 0, st, p, nch, npan);
+    else if (p.act == ACT_RELU) hipLaunchKernelGGL((panel_gemm_kernel<E_STORE, ACT_RELU, false>), g, b, 0, st, p, nch, npan);
+    else hipLaunchKernelGGL((panel_gemm_kernel<E_STORE, ACT_NONE, false>), g, b, 0, st, p, nch, npan);
   }
   return hipGetLastError();
 }

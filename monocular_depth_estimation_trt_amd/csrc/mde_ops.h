@@ -150,8 +150,8 @@ int gemm_store_split_slices(const GemmParams& p);
 bool conv_direct_supported(const GemmParams& p);
 hipError_t launch_conv3(const GemmParams& p, hipStream_t st);
 
-// A-stationary panel GEMM (gemm_panel.hip) for K = 384 token-major E_STORE
-// problems at large batch (the ViT-S fc1); launch_gemm routes there when
+// A-stationary panel GEMM (gemm_panel.hip) for K = 384 token-major E_STORE /
+// E_QKV problems at large batch (the ViT-S fc1 and qkv); launch_gemm routes there when
 // panel_gemm_eligible() (switch "panel").
 bool panel_gemm_eligible(const GemmParams& p);
 hipError_t launch_panel_gemm(const GemmParams& p, hipStream_t st);

@@ -38,8 +38,8 @@ enum Knob : int {
   // 1: 16 x 16-pixel tiles on 8 waves, 2: 8 x 16 on 4 waves).
   // test_conv_persist_bit_exact
   KNOB_CONV_PERSIST,
-  // A-stationary panel GEMM (gemm_panel.hip) for the K = 384 E_STORE
-  // problems at large batch -- the ViT-S fc1 (1: on).  test_panel_gemm_bit_exact
+  // A-stationary panel GEMM (gemm_panel.hip) for the K = 384 E_STORE /
+  // E_QKV problems at large batch -- the ViT-S fc1 and qkv (1: on).  test_panel_gemm_bit_exact
   KNOB_PANEL,
   KNOB_COUNT
 };

@@ -105,8 +105,9 @@ def test_panel_gemm_bit_exact(gpu, case):
     128^2 BK 32 kernel it replaces for K = 384 E_STORE at large M: the same
     MFMA k order and the same fp32 epilogue operations (LN statistics through
     the shared ln_merge_stats), so every output must be equal bit for bit,
-    with M not a multiple of 256.  The qkv cases (E_QKV stays on the 128^2
-    kernel) pin that the switch leaves them alone."""
+    with M not a multiple of 256 -- the E_STORE cases and the qkv head split
+    (q scaled, k, and V^T at its key-permuted positions; T = 37 puts image
+    boundaries inside every panel)."""
     from monocular_depth_estimation_trt_amd import _lib
     k = 384
     if case.startswith("linear") or case.startswith("lnfold"):
