@@ -102,8 +102,8 @@ const char* mde_last_error(void);
  * GEMM tiles (0 never, 1 auto, 2 always); "deep64" (0-1, 1) 4-deep ring for
  * small-grid 64^2 tiles; "w8small" (0-1, 1) 8-wave small-grid 128^2 tiles;
  * "conv_persist" (0-2, 1) persistent 64-channel RCU conv (1: 16 x 16 tiles,
- * 2: 8 x 16); "panel" (0-1, 1) A-stationary panel GEMM for the K = 384
- * qkv / fc1 at large batch.  The environment variable of a switch is exactly
+ * 2: 8 x 16); "panel" (0-2, 1) A-stationary panel GEMM for the K = 384
+ * qkv / fc1 at large batch (2: also the f16-residual proj).  The environment variable of a switch is exactly
  * MDE_ + its name upper-cased (MDE_DEEP64, MDE_W8SMALL, ...); a value that is
  * not an integer in range is reported on stderr and ignored.
  * Every setting computes the same depth map within the stated tolerance; the

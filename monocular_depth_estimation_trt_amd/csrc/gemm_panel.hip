@@ -133,9 +133,10 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
   const int nu = (int)((long long)(blockIdx.x + 1) * U / gridDim.x) - u0;
 
   // per-column bias and folded-LN column sums, read by every epilogue
+  // (E_RESID: tab_c holds the layer scale instead)
   for (int i = tid; i < p.N; i += 512) {
     tab_b[i] = p.bias ? p.bias[i] : 0.f;
-    tab_c[i] = FOLD ? p.lnc1[i] : 0.f;
+    tab_c[i] = FOLD ? p.lnc1[i] : (EM == E_RESID ? p.ls[i] : 0.f);
   }
 
   // ---- W chunk DMA: wave w fills rows 8w .. 8w + 7 of every 128-B row
@@ -199,8 +200,24 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
     const int n = c * PBN + jb * 16 + hq * 4;
     ColB r;
     r.b = *reinterpret_cast<const float4*>(tab_b + n);
-    r.c = FOLD ? *reinterpret_cast<const float4*>(tab_c + n) : float4{0.f, 0.f, 0.f, 0.f};
+    r.c = (FOLD || EM == E_RESID) ? *reinterpret_cast<const float4*>(tab_c + n) : float4{0.f, 0.f, 0.f, 0.f};
     return r;
+  };
+  // E_RESID: the f16 residual values a unit's epilogue updates, loaded during
+  // that unit (after its chunk DMA, drained by its end-of-unit wait) and
+  // consumed by the epilogue in the next unit -- a load consumed inside the
+  // unit that issued it would wait for the (older) chunk DMA as well
+  f16x4 rres[8];
+  auto res_load2 = [&](int b0, int pnl, int c) __attribute__((always_inline)) {  // blocks b0, b0 + 1
+    if constexpr (EM == E_RESID) {
+#pragma unroll
+      for (int b = b0; b < b0 + 2; ++b) {
+        const int m = row_of(pnl, b >> 2);
+        const int mr = m < p.M ? m : p.M - 1;
+        rres[b] = *reinterpret_cast<const f16x4*>(reinterpret_cast<const f16*>(p.xh) + (size_t)mr * p.ldo + c * PBN +
+                                                  (b & 3) * 16 + hq * 4);
+      }
+    }
   };
   // the 4 outputs of block (ib, jb) of unit (pnl, c), one rounding to f16;
   // rows >= M and the dummy epilogue of a run's first unit go to the sink.
@@ -208,14 +225,22 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
   // of q, k or v): q (scaled) / k rows [b*heads + h][t][64] take the 8 B at
   // dh .. dh+3; V^T [b*heads + h][64][Tpad] takes 4 scalar stores at key
   // position vt_pos(t) of rows dh .. dh+3
-  auto store4 = [&](int ib, int jb, int pnl, int c, float y0, float y1, float y2, float y3, bool live)
-                    __attribute__((always_inline)) {
+  auto store4 = [&](int ib, int jb, int pnl, int c, float y0, float y1, float y2, float y3, bool live,
+                    const float4& ls) __attribute__((always_inline)) {
     const int m = row_of(pnl, ib);
     const bool ok = live && m < p.M;
+    f16x4 h = {(f16)y0, (f16)y1, (f16)y2, (f16)y3};
     if constexpr (EM == E_STORE) {
-      const f16x4 h = {(f16)y0, (f16)y1, (f16)y2, (f16)y3};
       const int n = c * PBN + jb * 16 + hq * 4;
       f16x4* dst = ok ? reinterpret_cast<f16x4*>(reinterpret_cast<f16*>(p.out16) + (size_t)m * p.ldo + n) : g_psink + lane;
+      *dst = h;
+    } else if constexpr (EM == E_RESID) {
+      // xh += ls * (acc + bias): fp32 update, one rounding (the 128^2 kernel's)
+      const f16x4 x = rres[ib * 4 + jb];
+      h = f16x4{(f16)((float)x[0] + ls.x * y0), (f16)((float)x[1] + ls.y * y1), (f16)((float)x[2] + ls.z * y2),
+                (f16)((float)x[3] + ls.w * y3)};
+      const int n = c * PBN + jb * 16 + hq * 4;
+      f16x4* dst = ok ? reinterpret_cast<f16x4*>(reinterpret_cast<f16*>(p.xh) + (size_t)m * p.ldo + n) : g_psink + lane;
       *dst = h;
     } else {
       const int which = c / p.heads, hh = c - which * p.heads;
@@ -224,7 +249,7 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
       const int dh = jb * 16 + hq * 4;
       if (which < 2) {
         const float sc = which == 0 ? p.qscale : 1.f;
-        const f16x4 h = {(f16)(y0 * sc), (f16)(y1 * sc), (f16)(y2 * sc), (f16)(y3 * sc)};
+        h = f16x4{(f16)(y0 * sc), (f16)(y1 * sc), (f16)(y2 * sc), (f16)(y3 * sc)};
         f16* base = which == 0 ? reinterpret_cast<f16*>(p.q) : reinterpret_cast<f16*>(p.k);
         f16x4* dst = ok ? reinterpret_cast<f16x4*>(base + ((size_t)(b * p.heads + hh) * p.Tpad + t) * 64 + dh)
                         : g_psink + lane;
@@ -233,32 +258,47 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
         f16* row = reinterpret_cast<f16*>(p.vt) + ((size_t)(b * p.heads + hh) * 64 + dh) * p.Tpad + vt_pos(t);
         f16* sink = reinterpret_cast<f16*>(g_psink + lane);
         const size_t tp = p.Tpad;
-        *(ok ? row : sink) = (f16)y0;
-        *(ok ? row + tp : sink) = (f16)y1;
-        *(ok ? row + 2 * tp : sink) = (f16)y2;
-        *(ok ? row + 3 * tp : sink) = (f16)y3;
+        *(ok ? row : sink) = h[0];
+        *(ok ? row + tp : sink) = h[1];
+        *(ok ? row + 2 * tp : sink) = h[2];
+        *(ok ? row + 3 * tp : sink) = h[3];
       }
     }
+    return h;
   };
-  auto epi_block = [&](int ib, int jb, int pnl, int c, const f32x4& a, float mean, float rstd, const ColB& cb,
-                       bool live) __attribute__((always_inline)) {
-    f32x4 v = a;
-    if constexpr (FOLD) {
-      const float nm = -rstd * mean;
-      v[0] = fmaf(rstd, v[0], nm * cb.c.x);
-      v[1] = fmaf(rstd, v[1], nm * cb.c.y);
-      v[2] = fmaf(rstd, v[2], nm * cb.c.z);
-      v[3] = fmaf(rstd, v[3], nm * cb.c.w);
-    }
-    v[0] += cb.b.x; v[1] += cb.b.y; v[2] += cb.b.z; v[3] += cb.b.w;
-    if constexpr (ACT == ACT_RELU) {
+  // E_RESID with lnst_out: the folded-LN partials of the f16 values written,
+  // per row and 32-column slice (sum, M2 about the slice mean): a block pair
+  // (jb, jb + 1) is one slice; the 4 lanes of a row (lane >> 4) hold its 32
+  // values.  Same definition as the 128^2 kernel's (tile_epilogue.h
+  // ln_partials); the summation groups differ, so equal to fp32 rounding.
+  auto ln_slice = [&](int ib, int pnl, int slice, const f16x4& h0, const f16x4& h1, bool live)
+                      __attribute__((always_inline)) {
+    float s1 = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) v[r] = v[r] > 0.f ? v[r] : 0.f;
-    } else if constexpr (ACT == ACT_GELU) {
-      const f32x2 lo = gelu_erf2(f32x2{v[0], v[1]}), hi = gelu_erf2(f32x2{v[2], v[3]});
-      v = f32x4{lo[0], lo[1], hi[0], hi[1]};
+    for (int r = 0; r < 4; ++r) s1 += (float)h0[r];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) s1 += (float)h1[r];
+    s1 += __shfl_xor(s1, 16);
+    s1 += __shfl_xor(s1, 32);
+    const float ms = s1 * (1.f / 32.f);
+    float s2 = 0.f;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float d = (float)h0[r] - ms;
+      s2 += d * d;
     }
-    store4(ib, jb, pnl, c, v[0], v[1], v[2], v[3], live);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      const float d = (float)h1[r] - ms;
+      s2 += d * d;
+    }
+    s2 += __shfl_xor(s2, 16);
+    s2 += __shfl_xor(s2, 32);
+    const int m = row_of(pnl, ib);
+    float2* dst = (live && m < p.M && hq == 0)
+                      ? reinterpret_cast<float2*>(p.lnst_out + ((size_t)slice * p.lnst_rows + m) * 2)
+                      : reinterpret_cast<float2*>(g_psink + lane);
+    *dst = make_float2(s1, s2);
   };
   // two blocks (2 x 4 values) in lockstep: each step of gelu_erf2 for all
   // four value pairs before the next (the same operations per value, so
@@ -309,10 +349,14 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
 #pragma unroll
       for (int q = 0; q < 4; ++q) y[q] = x[q];
     }
+    f16x4 hw[2];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
       const int b = b0 + e, ib = b >> 2, jb = b & 3;
-      store4(ib, jb, pnl, c, y[2 * e][0], y[2 * e][1], y[2 * e + 1][0], y[2 * e + 1][1], live);
+      hw[e] = store4(ib, jb, pnl, c, y[2 * e][0], y[2 * e][1], y[2 * e + 1][0], y[2 * e + 1][1], live, cb[e].c);
+    }
+    if constexpr (EM == E_RESID) {
+      if (p.lnst_out) ln_slice(b0 >> 2, pnl, c * 2 + ((b0 & 3) >> 1), hw[0], hw[1], live);
     }
   };
 
@@ -324,23 +368,30 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
   // beside its substep's 8 MFMAs.
   const int cx = (hq ^ (lane & 7)) << 4;  // physical chunk of logical chunk hq in rows r (r & 7 = lane & 7)
   auto unit = [&](auto off_tag, int j, f32x4(&accC)[2][4], const f32x4(&accP)[2][4], bool epi, int ppnl, int pc,
-                  const float (&pmean)[2], const float (&prstd)[2]) __attribute__((always_inline)) {
+                  const float (&pmean)[2], const float (&prstd)[2], int cpnl, int cc) __attribute__((always_inline)) {
     constexpr int OFF = decltype(off_tag)::value;
     const char* sw = smem + (j & 1) * PCHB + l15 * 128;
 #pragma unroll
     for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb) accC[ib][jb] = f32x4{0.f, 0.f, 0.f, 0.f};
-    f16x8 wf[2][4];
+    // (E_RESID: one set -- its residual values take the 16 VGPRs of the
+    // second; the fragments are then read at the top of their own substep)
+    constexpr int WB = EM == E_RESID ? 1 : 2;
+    f16x8 wf[WB][4];
     auto rd = [&](int s, f16x8(&w)[4]) __attribute__((always_inline)) {
       const int off = (s >> 1) * 8192 + (cx ^ ((s & 1) << 6));  // logical chunk 4 (s & 1) + hq
 #pragma unroll
       for (int jb = 0; jb < 4; ++jb) w[jb] = *reinterpret_cast<const f16x8*>(sw + off + jb * 2048);
     };
-    rd(0, wf[0]);
+    if constexpr (WB == 2) rd(0, wf[0]);
 #pragma unroll
     for (int s = 0; s < PKS; ++s) {
-      if (s + 1 < PKS) rd(s + 1, wf[(s + 1) & 1]);
+      if constexpr (WB == 2) {
+        if (s + 1 < PKS) rd(s + 1, wf[(s + 1) & 1]);
+      } else {
+        rd(s, wf[0]);
+      }
       // the epilogue's 4 block pairs run in substeps OFF, OFF + E, .. OFF + 3E
       constexpr int E = PEPI_STRIDE;
       const bool ep = s >= OFF && ((s - OFF) % E) == 0 && (s - OFF) / E < 4;
@@ -350,10 +401,15 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
 #pragma unroll
       for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
-        for (int jb = 0; jb < 4; ++jb) accC[ib][jb] = mfma16x16x32(wf[s & 1][jb], af[ib][s], accC[ib][jb]);
+        for (int jb = 0; jb < 4; ++jb) accC[ib][jb] = mfma16x16x32(wf[s % WB][jb], af[ib][s], accC[ib][jb]);
       // blocks 2s, 2s + 1 of the previous unit in substeps 0 .. 3: its stores
       // are then at least 8 substeps old at the end-of-unit wait
-      if (ep) epi_pair(2 * q, ppnl, pc, accP, pmean, prstd, cb, epi);
+      if (ep) {
+        epi_pair(2 * q, ppnl, pc, accP, pmean, prstd, cb, epi);
+        // (E_RESID) those two blocks' registers now take this unit's
+        // residual values -- landed by the end-of-unit wait, used next unit
+        res_load2(2 * q, cpnl, cc);
+      }
       __builtin_amdgcn_sched_barrier(0);
     }
   };
@@ -378,9 +434,10 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
     // outer loop: one run of units per A panel (af loop-invariant inside)
     auto epi_all = [&]() __attribute__((always_inline)) {  // a unit's whole epilogue, standalone
 #pragma unroll
-      for (int b = 0; b < 8; ++b)
-        epi_block(b >> 2, b & 3, ppnl, pc, acc1[b >> 2][b & 3], lmean[b >> 2], lrstd[b >> 2], col_read(pc, b & 3),
-                  true);
+      for (int q = 0; q < 4; ++q) {
+        const ColB cb[2] = {col_read(pc, (2 * q) & 3), col_read(pc, (2 * q + 1) & 3)};
+        epi_pair(2 * q, ppnl, pc, acc1, lmean, lrstd, cb, true);
+      }
     };
     int j = 0;
     while (j < nu) {
@@ -399,7 +456,7 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
         // fixed accumulator roles and a copy per unit (32 moves per 96
         // MFMAs): alternating the two sets by unit parity left both live
         // across a branch and spilled
-        unit(off_tag, j, acc0, acc1, j > j0, pnl, pc, lmean, lrstd);
+        unit(off_tag, j, acc0, acc1, j > j0, pnl, pc, lmean, lrstd, pnl, (u0 + j) - pnl * nch);
 #pragma unroll
         for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
@@ -439,7 +496,8 @@ extern "C" int mde_debug_panel_trace(unsigned long long* host) {
 
 bool panel_gemm_eligible(const GemmParams& p) {
   if (!knob(KNOB_PANEL)) return false;
-  if (p.amode != A_DENSE || p.K != PK || p.a_tok != 0 || p.lnst_out || p.splitk > 1) return false;
+  if (p.amode != A_DENSE || p.K != PK || p.a_tok != 0 || (p.lnst_out && p.emode != E_RESID) || p.splitk > 1)
+    return false;
   if (p.N % PBN || p.N > PNMAX || (p.lda & 7) || p.lda < PK || p.ldw < PK || (p.ldw & 63)) return false;
   if (p.lnst_in && (!p.lnc1 || p.lnst_ns != PK / 32 || p.lnst_rows != p.M)) return false;
   // whole CUs of work: at least 64 panels (B >= 12 ViT-S images)
@@ -447,6 +505,13 @@ bool panel_gemm_eligible(const GemmParams& p) {
   if (p.emode == E_STORE)
     return p.out16 && !p.res0 && !p.res1 && !(p.ldo & 3) && !((uintptr_t)p.out16 & 7) && p.ldo >= p.N &&
            (p.act == ACT_NONE || p.act == ACT_RELU || p.act == ACT_GELU);
+  // the f16-residual form (DA-V2 fp16 engines), no LN fold on its input: only
+  // at "panel" = 2 -- bit-exact but slower than the whole-row 128 x 384 tile
+  // in the engine (N = 384 gives 6 units per panel: the panel switch is not
+  // amortised)
+  if (p.emode == E_RESID)
+    return knob(KNOB_PANEL) == 2 && p.xh && p.ls && !p.lnst_in && !(p.ldo & 3) && !((uintptr_t)p.xh & 7) && p.ldo >= p.N && !p.partial &&
+           (!p.lnst_out || (p.lnst_ns * 32 == p.N && p.lnst_rows >= p.M));
   if (p.emode == E_QKV)
     return p.heads > 0 && p.heads * 64 * 3 == p.N && p.T > 0 && p.Tpad >= p.T && p.q && p.k && p.vt &&
            !((uintptr_t)p.q & 7) && !((uintptr_t)p.k & 7) && p.act == ACT_NONE;
@@ -458,7 +523,9 @@ hipError_t launch_panel_gemm(const GemmParams& p, hipStream_t st) {
   const int U = nch * npan;
   const int G = U < cu_count() ? U : cu_count();
   const dim3 g(G), b(512);
-  if (p.emode == E_QKV) {
+  if (p.emode == E_RESID) {
+    hipLaunchKernelGGL((panel_gemm_kernel<E_RESID, ACT_NONE, false>), g, b, 0, st, p, nch, npan);
+  } else if (p.emode == E_QKV) {
     if (p.lnst_in) hipLaunchKernelGGL((panel_gemm_kernel<E_QKV, ACT_NONE, true>), g, b, 0, st, p, nch, npan);
     else hipLaunchKernelGGL((panel_gemm_kernel<E_QKV, ACT_NONE, false>), g, b, 0, st, p, nch, npan);
   } else if (p.lnst_in) {

@@ -39,7 +39,8 @@ enum Knob : int {
   // test_conv_persist_bit_exact
   KNOB_CONV_PERSIST,
   // A-stationary panel GEMM (gemm_panel.hip) for the K = 384 E_STORE /
-  // E_QKV problems at large batch -- the ViT-S fc1 and qkv (1: on).  test_panel_gemm_bit_exact
+  // E_QKV problems at large batch -- the ViT-S fc1 and qkv (1: on; 2: also
+  // the f16-residual proj, slower in the engine).  test_panel_gemm_bit_exact
   KNOB_PANEL,
   KNOB_COUNT
 };

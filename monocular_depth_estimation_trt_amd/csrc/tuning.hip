@@ -28,7 +28,7 @@ constexpr KnobDef kKnobs[KNOB_COUNT] = {
     {"deep64", "MDE_DEEP64", 1, 0, 1},
     {"w8small", "MDE_W8SMALL", 1, 0, 1},
     {"conv_persist", "MDE_CONV_PERSIST", 1, 0, 2},
-    {"panel", "MDE_PANEL", 1, 0, 1},
+    {"panel", "MDE_PANEL", 1, 0, 2},
 };
 
 std::atomic<int> g_val[KNOB_COUNT];

@@ -98,7 +98,7 @@ def test_qkv_layout(gpu, B, T, H):
 
 
 @pytest.mark.parametrize("case", ["linear_gelu", "linear_none", "linear_relu_tail", "lnfold_gelu",
-                                  "qkv_1370", "qkv_37", "qkv_lnfold"])
+                                  "qkv_1370", "qkv_37", "qkv_lnfold", "resid_proj", "resid_proj_tail"])
 def test_panel_gemm_bit_exact(gpu, case):
     """Switch "panel" (gemm_panel.hip: A-stationary 256-row panels, each
     unit's MFMAs interleaved with the previous unit's epilogue) against the
@@ -110,6 +110,30 @@ def test_panel_gemm_bit_exact(gpu, case):
     boundaries inside every panel)."""
     from monocular_depth_estimation_trt_amd import _lib
     k = 384
+    if case.startswith("resid"):
+        # proj over the f16 residual stream: xh must match bit for bit; the
+        # LN partials of the rows written sum the same 32 f16 values in
+        # another grouping, so they agree to fp32 rounding
+        m, n = (65760, 384) if case == "resid_proj" else (16397, 384)
+        a = (rn(m, k) * 2).half().to(gpu)
+        w, b = rn(n, k, scale=k ** -0.5), rn(n, scale=0.1).to(gpu)
+        ls = (0.5 + 0.1 * rn(n)).to(gpu)
+        wp = pad_w(w).to(gpu)
+        x0 = (rn(m, n) * 2).half().to(gpu)
+        res = []
+        for panel in (2, 0):  # proj takes the panel kernel only at panel = 2
+            xh = x0.clone()
+            part = torch.full((n // 32, m, 2), float("nan"), device=gpu)
+            with _lib.tuning(panel=panel):
+                op("mde_op_linear_residual_f16", ptr(a), k, ptr(wp), wp.shape[1], m, n, k, ptr(b), ptr(ls), ptr(xh), n,
+                   ptr(part), stream())
+            res.append((xh, part))
+        d = (res[0][0].float() - res[1][0].float()).abs()
+        assert torch.equal(res[0][0], res[1][0]), \
+            f"{case}: xh differs ({int((d > 0).sum())} elements, max {float(d.max())})"
+        assert torch.isfinite(res[0][1]).all(), "partials not all written"
+        close(res[0][1], res[1][1].float(), 1e-5, 1e-4, f"{case} ln partials")
+        return
     if case.startswith("linear") or case.startswith("lnfold"):
         m = {"linear_gelu": 16384, "linear_none": 21920, "linear_relu_tail": 16397, "lnfold_gelu": 38360}[case]
         n = 1536 if case != "linear_none" else 1152

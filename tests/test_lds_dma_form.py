@@ -1,9 +1,13 @@
 """Every LDS-DMA in the product library uses the 64-bit-address form
-(`global_load_lds_dwordx4 v[a:b], off`).  The SADDR (`v, s[..]`) and MUBUF
-(`buffer_load ... lds`) forms take a 32-bit offset register; with them a
-ds_read destination reusing that register gave nondeterministic outputs in
-round 4's fused-MLP experiment (tools/dma_hazard_scan.py).
-CPU only: disassembles the device code of the in-tree build's objects."""
+(`global_load_lds_dwordx4 v[a:b], off`), except the panel GEMM
+(gemm_panel.hip), whose DMAs take the SADDR form (`v, s[..]`: SGPR base + a
+32-bit VGPR offset, so no 64-bit address pair is live across its loop).  A
+ds_read destination reusing the offset register of an in-flight DMA was the
+suspect of round 4's nondeterministic fused-MLP experiment; the round-5 probe
+(tools/dma_war_probe.hip, profiles/r05_dma_war_probe.json) found the SADDR
+form as safe as the vaddr form, and the second test below requires that no
+reuse site of a non-vaddr form exists anyway.  The MUBUF `... lds` form stays
+out.  CPU only: disassembles the device code of the in-tree build's objects."""
 import glob
 import os
 import re
@@ -36,7 +40,8 @@ def test_product_lds_dma_uses_the_64bit_address_form():
         finally:
             shutil.rmtree(d)
         seen += len(re.findall(r"global_load_lds_dword\w*", txt))
-        assert not re.findall(r"global_load_lds_dword\w*\s+v\d+, s\[", txt), src
+        if src != "gemm_panel.hip":
+            assert not re.findall(r"global_load_lds_dword\w*\s+v\d+, s\[", txt), src
         assert not re.findall(r"buffer_load_\w+[^\n]*\blds\b", txt), src
     assert seen > 0
 
@@ -57,7 +62,7 @@ def test_product_has_no_unclear_dma_address_reuse():
         findings += f
         cleared += c
     assert not findings, findings[:5]
-    assert all(S.dma_form(h[1]) == "vaddr64" for h in cleared)
+    assert all(S.dma_form(h[1]) == "vaddr64" for h in cleared), [h for h in cleared if S.dma_form(h[1]) != "vaddr64"][:5]
 
 
 def test_dma_scanner_flags_the_probe_patterns():

@@ -17,7 +17,8 @@ ds_read overwriting the address registers as the very next instruction
 queues stay full) returned 0 wrong rows for the 64-bit vaddr form, the
 SADDR form and the MUBUF `offen lds` form alike, while the positive control
 (decoy address in the registers before the issue) returned the decoy on every
-lane.  The product keeps the 64-bit vaddr form anyway (tests/test_lds_dma_form.py);
+lane.  The product keeps the 64-bit vaddr form anyway except in the panel
+GEMM (SADDR form, no reuse site allowed; tests/test_lds_dma_form.py);
 a reuse site behind any OTHER form is reported as a finding (exit 1), the
 vaddr-form sites as cleared by the probe (listed with --list).
 

@@ -10,6 +10,7 @@
 #   peak                  tools/mfma_peak.hip (f16 MFMA peak)         -> OUT/mfma_peak.json
 #   probe[:ITERS,LAUNCHES] tools/dma_war_probe.hip (LDS-DMA address WAR) -> OUT/dma_war_probe.json
 #   bench:TAG:ARGS        python bench.py ARGS (ARGS comma-separated) -> OUT/bench_TAG.json/.err
+#   benchlib:TAG:LIB,ARGS bench.py ARGS against variant library LIB -> OUT/bench_TAG.json/.err
 #   profile:TAG:ARGS      tools/profile_round.sh (stats + FETCH/WRITE passes) -> OUT/prof_TAG/
 #   pmc:TAG:ARGS          tools/pmc_profile.sh on bench.py ARGS (SQ/TCC passes) -> OUT/pmc_TAG/
 #   kpmc:TAG:ARGS         tools/pmc_profile.sh on tools/bench_kernels.py ARGS    -> OUT/kpmc_TAG/
@@ -45,6 +46,9 @@ for t in "$@"; do
     bench)
       timeout -k 10 600 python -u bench.py "${args[@]}" > "$O/bench_$tag.json" 2> "$O/bench_$tag.err" \
         || { log "bench rc=$?"; tail -20 "$O/bench_$tag.err"; exit 1; } ;;
+    benchlib)  # benchlib:TAG:LIB,ARGS -- bench.py against a variant library
+      timeout -k 10 600 python -u tools/bench_lib.py "${args[@]}" > "$O/bench_$tag.json" 2> "$O/bench_$tag.err" \
+        || { log "benchlib rc=$?"; tail -20 "$O/bench_$tag.err"; exit 1; } ;;
     profile)
       bash tools/profile_round.sh "$O/prof_$tag" "${args[@]}" || { log "profile rc=$?"; exit 1; } ;;
     pmc)
