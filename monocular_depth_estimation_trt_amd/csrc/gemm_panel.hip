@@ -474,6 +474,8 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
   else run(std::integral_constant<int, PEPI_OFF1>{});
 }
 
+}  // namespace
+
 int cu_count() {
   static int n = 0;
   if (n == 0) {
@@ -485,8 +487,6 @@ int cu_count() {
   }
   return n;
 }
-
-}  // namespace
 
 #ifdef PX_TRACE
 extern "C" int mde_debug_panel_trace(unsigned long long* host) {

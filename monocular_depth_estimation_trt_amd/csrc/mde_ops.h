@@ -154,6 +154,8 @@ hipError_t launch_conv3(const GemmParams& p, hipStream_t st);
 // E_QKV problems at large batch (the ViT-S fc1 and qkv); launch_gemm routes there when
 // panel_gemm_eligible() (switch "panel").
 bool panel_gemm_eligible(const GemmParams& p);
+// compute units of the current device (cached)
+int cu_count();
 hipError_t launch_panel_gemm(const GemmParams& p, hipStream_t st);
 
 // 256x256 phase-pipelined dense GEMM (gemm256.hip) for large token-major
