@@ -370,11 +370,16 @@ def test_patch_embed(gpu, B, Hh, Ww):
     w16 = torch.zeros(D, 3, 14, 16)
     w16[..., :14] = w
     wp = pad_w(w16.reshape(D, 672)).to(gpu)
-    scratch = torch.empty(B * ph * pw, 672, dtype=torch.float16, device=gpu)
+    scratch = torch.full((B * ph * pw, 672), float("nan"), dtype=torch.float16, device=gpu)
     x = torch.empty(B * (ph * pw + 1), D, device=gpu)
     op("mde_op_patch_embed", ptr(img.to(gpu)), B, Hh, Ww, ptr(wp), wp.shape[1], ptr(b.to(gpu)), ptr(pos.to(gpu)),
        ptr(cls_pos.to(gpu)), D, ptr(scratch), ptr(x), stream())
     close(x, ref, 1e-3, 2e-3, "patch_embed")
+    # the gathered patch matrix itself, exactly: [patch][c][ky][16] f16 of the
+    # image, columns 14 and 15 of every kernel row zero
+    pm = torch.zeros(B, ph, pw, 3, 14, 16, dtype=torch.float16)
+    pm[..., :14] = img.half().reshape(B, 3, ph, 14, pw, 14).permute(0, 2, 4, 1, 3, 5)
+    assert torch.equal(scratch.cpu(), pm.reshape(B * ph * pw, 672)), "patch matrix differs"
 
 
 @pytest.mark.parametrize("B,h,w,cin,cout,stride,relu_in,act,nres", [
