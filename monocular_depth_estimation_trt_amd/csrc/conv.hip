@@ -739,6 +739,12 @@ constexpr int UTH = 16, UTW = 16;                        // output tile
 constexpr int UPH = UTH + 2, UPW = UTW + 2;              // virtual patch
 constexpr int USR = 13;                                  // source rows per tile (host-checked)
 constexpr int UPATCH = UPH * UPW * 64, UHBUF = USR * UPW * 64;
+// byte offset of (row, column, logical 16-B chunk) in the patch / H buffers:
+// rows of UPW pixels x 64 B, the chunk swizzled by the COLUMN only (within a
+// row the same bank spread as a pixel-index swizzle; across rows a pure
+// offset, so the 3 x 3 taps' row steps fold into ds_read immediates and a
+// lane needs one base address per column shift)
+MDE_DEV int uoff(int row, int col, int lc) { return row * (UPW * 64) + col * 64 + ((lc ^ ((col >> 1) & 3)) << 4); }
 
 template <int NCH, int EM, bool PERSIST>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NCH == 1 ? 6 : 4)))
@@ -860,8 +866,7 @@ upconv_kernel(const GemmParams p) {
 #pragma unroll
     for (int k = 0; k < HI; ++k) {
       if (hs[k]) {
-        const int hp = (rg + k * RG) * UPW + col;
-        *reinterpret_cast<f16x8*>(sH + hp * 64 + cpch<32>(hp, lc) * 16) =
+        *reinterpret_cast<f16x8*>(sH + uoff(rg + k * RG, col, lc)) =
             hin ? lerp8(ha[k], hb[k], hw) : zero8();
       }
     }
@@ -912,14 +917,12 @@ upconv_kernel(const GemmParams p) {
           int y0, y1;
           float ly0, ly1;
           ac_index(usy, iy, p.ch, y0, y1, ly0, ly1);
-          const int h0 = (y0 - g.sy0) * UPW + col, h1 = (y1 - g.sy0) * UPW + col;
-          const f16x8 a = *reinterpret_cast<const f16x8*>(sH + h0 * 64 + cpch<32>(h0, lc) * 16);
-          const f16x8 bb = *reinterpret_cast<const f16x8*>(sH + h1 * 64 + cpch<32>(h1, lc) * 16);
+          const f16x8 a = *reinterpret_cast<const f16x8*>(sH + uoff(y0 - g.sy0, col, lc));
+          const f16x8 bb = *reinterpret_cast<const f16x8*>(sH + uoff(y1 - g.sy0, col, lc));
           v = lerp8(a, bb, (f16)ly1);
           if (p.relu_in) v = relu8(v);
         }
-        const int pp = r * UPW + col;
-        *reinterpret_cast<f16x8*>(sP + pp * 64 + cpch<32>(pp, lc) * 16) = v;
+        *reinterpret_cast<f16x8*>(sP + uoff(r, col, lc)) = v;
       }
     }
     __syncthreads();
@@ -932,8 +935,7 @@ upconv_kernel(const GemmParams p) {
         f16x8 fa[TM], fb[TN];
 #pragma unroll
         for (int i = 0; i < TM; ++i) {
-          const int pp = (wave * TM + i + ky) * UPW + (lane & 15) + kx;
-          fa[i] = *reinterpret_cast<const f16x8*>(sP + pp * 64 + cpch<32>(pp, lc) * 16);
+          fa[i] = *reinterpret_cast<const f16x8*>(sP + uoff(wave * TM + i + ky, (lane & 15) + kx, lc));
         }
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
