@@ -737,7 +737,10 @@ bool conv64p_launch(const GemmParams& p, hipStream_t st, hipError_t& err) {
 // workgroups per CU.
 constexpr int UTH = 16, UTW = 16;                        // output tile
 constexpr int UPH = UTH + 2, UPW = UTW + 2;              // virtual patch
-constexpr int USR = 13;                                  // source rows per tile (host-checked)
+// source rows per tile (host-checked, exactly): 12 keeps the cc = 32 kernel
+// at 52 KB of LDS -- three workgroups per CU also at the hardware's LDS
+// allocation granule (13 rows, 53.1 KB, measured 3.1 resident waves per SIMD)
+constexpr int USR = 12;
 constexpr int UPATCH = UPH * UPW * 64, UHBUF = USR * UPW * 64;
 // byte offset of (row, column, logical 16-B chunk) in the patch / H buffers:
 // rows of UPW pixels x 64 B, the chunk swizzled by the COLUMN only (within a
@@ -1031,15 +1034,28 @@ upconv_kernel(const GemmParams p) {
 // switch "upconv" = 0: the upsampling convs stay on conv3_kernel (A/B, tests)
 bool upconv_enabled() { return knob(KNOB_UPCONV) != 0; }
 
-// a 16-row tile's 18 virtual rows must come from at most USR source rows:
-// (UPH - 1) * scale + 2 rows, with a one-row margin for the float index
+// every 16-row tile's 18 virtual rows must come from at most USR source
+// rows: the device's fp32 index arithmetic (ac_scale, ac_index in geo())
+// restated on the host for each tile row -- the exact span, not a bound
 bool upconv_eligible(const GemmParams& p) {
+#pragma clang fp contract(off)
   if (p.amode != A_CONV3_UP || p.N != 32 || p.stride != 1 || (p.cc & 31) || p.cc > 128) return false;
   if (p.emode != E_STORE && p.emode != E_HEAD) return false;
   if (p.emode == E_STORE && ((p.ldo & 3) || p.res0 || p.res1)) return false;
-  if (p.uh < 2 || p.uw < 1 || p.ch < 1 || p.cw < 1) return false;
-  const double sy = (double)(p.ch - 1) / (double)(p.uh - 1);
-  return sy * (UPH - 1) + 3.0 <= (double)USR && upconv_enabled();
+  if (p.uh < 2 || p.uw < 1 || p.ch < 1 || p.cw < 1 || p.oh != p.uh) return false;
+  if (!upconv_enabled()) return false;
+  const float sy = (float)(p.ch - 1) / (float)(p.uh - 1);
+  const int tiles_y = (p.oh + UTH - 1) / UTH;
+  for (int ty = 0; ty < tiles_y; ++ty) {
+    const int iy0 = ty * UTH - 1;
+    const int first = iy0 < 0 ? 0 : iy0;
+    const int last = iy0 + UPH - 1 < p.uh - 1 ? iy0 + UPH - 1 : p.uh - 1;
+    const int a0 = (int)(sy * (float)first);
+    const int l0 = (int)(sy * (float)last);
+    const int b1 = l0 + (l0 < p.ch - 1 ? 1 : 0);
+    if (b1 - a0 + 1 > USR) return false;
+  }
+  return true;
 }
 
 // persistent grid: workgroups per CU the LDS allows x 256 CUs (grids up to
