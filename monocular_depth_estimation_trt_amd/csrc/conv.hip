@@ -972,17 +972,23 @@ upconv_kernel(const GemmParams p) {
               const int n0 = j * 16 + (vl >> 4) * 4;
               const float4 bn = *reinterpret_cast<const float4*>(sBias + n0);
               const float4 w2 = *reinterpret_cast<const float4*>(sBias + 32 + n0);
-              float pv[4] = {0.f, 0.f, 0.f, 0.f};
+              float h0 = acc[i][j][0] + bn.x, h1 = acc[i][j][1] + bn.y;
+              float h2 = acc[i][j][2] + bn.z, h3 = acc[i][j][3] + bn.w;
               if constexpr (PE) {
+                // (+ 0 where no embedding: the no-PE path skips the add -- it
+                // changes only a -0 sum, which the ReLU below maps to +0 anyway)
+                float pv[4] = {0.f, 0.f, 0.f, 0.f};
                 if (m >= 0) {
                   const f16x4 q = *reinterpret_cast<const f16x4*>(reinterpret_cast<const f16*>(p.hpe) +
                                                                   (size_t)(m % p.hpe_pix) * 32 + n0);
 #pragma unroll
                   for (int r = 0; r < 4; ++r) pv[r] = (float)q[r];
                 }
+                h0 += pv[0];
+                h1 += pv[1];
+                h2 += pv[2];
+                h3 += pv[3];
               }
-              const float h0 = acc[i][j][0] + bn.x + pv[0], h1 = acc[i][j][1] + bn.y + pv[1];
-              const float h2 = acc[i][j][2] + bn.z + pv[2], h3 = acc[i][j][3] + bn.w + pv[3];
               // explicit fma chain: the contraction store_tile's loop gets
               // (packed-math vectorisation would otherwise split some of it)
               part = fmaf(h0 > 0.f ? h0 : 0.f, w2.x, part);
