@@ -545,6 +545,13 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
         if (p.K <= kBk32Kmax) return run<128, 128, 2, 2, AM, EM, 32>(p, st);
         if (w8small(big)) return run<128, 128, 2, 4, AM, EM>(p, st);
       }
+      // the patch embed (K 672) and the resize-layer ConvTs (K 48 / 96) too:
+      // ViT-S B = 48, per layer, two same-box runs: patch_embed 86.4 / 85.8 ->
+      // 83.5 / 83.8 us, convT4 57.8 / 59.1 -> 48.6 / 50.6, convT2 34.7 / 34.8
+      // -> 31.4 / 32.4 (profiles/r05_patch_convt_bk32.txt)
+      if constexpr (AM == A_DENSE && (EM == E_PATCH || EM == E_CONVT)) {
+        if (p.K <= kBk32Kmax) return run<128, 128, 2, 2, AM, EM, 32>(p, st);
+      }
       return run<128, 128, 2, 2, AM, EM>(p, st);
     }
     if constexpr (AM == A_DENSE) {
