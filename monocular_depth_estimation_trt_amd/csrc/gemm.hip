@@ -602,11 +602,20 @@ int store_split_slices(const GemmParams& p) {
   // at least 12 K-steps: the 64-channel convs of the ViT-S DPT (K 576, 9
   // steps) run better unsplit (ViT-S B=1 0.925 -> 0.902 ms per forward with
   // 12 vs 8; 16: 0.909)
-  if (wgs >= 256 || nk < 12) return 1;
-  // fill two workgroups per CU without spilling into a third: the slices then
-  // run the 4-deep ring (deep64), which a 513th workgroup would forfeit
-  int S = (int)((512 + t64 - 1) / t64);
-  if (512 / t64 >= 2) S = (int)(512 / t64);  // (independent of the "deep64" switch: same slices either way)
+  if (nk < 12) return 1;
+  int S;
+  if (wgs >= 256) {
+    // a grid just over one workgroup per CU with a long K loop -- ViT-S B =
+    // 48 layer4_rn, 271 64^2 tiles x 54 K-steps, 43 us at one workgroup per
+    // CU -- takes two slices (2-stage ring, all resident)
+    if (wgs >= 384 || nk < 48) return 1;
+    S = 2;
+  } else {
+    // fill two workgroups per CU without spilling into a third: the slices then
+    // run the 4-deep ring (deep64), which a 513th workgroup would forfeit
+    S = (int)((512 + t64 - 1) / t64);
+    if (512 / t64 >= 2) S = (int)(512 / t64);  // (independent of the "deep64" switch: same slices either way)
+  }
   S = S < nk / 4 ? S : nk / 4;  // >= 4 K-steps per slice
   S = S < 16 ? S : 16;
   while (S > 1 && (size_t)S * p.M * p.N > p.partial_cap) --S;
