@@ -33,7 +33,11 @@
 //    (panel, chunk) units, so a panel's A is loaded once or twice per CU.
 //
 // Reference ops covered: a9 qkv, a12 fc1 + GELU (the a8 / a10
-// LayerNorms folded).
+// LayerNorms folded).  The f16-residual form (proj: xh += ls * (.), with the
+// LN partials of the rows written) is built too but taken only at switch
+// "panel" = 2: at N = 384 a panel has 6 units and its load is not amortised
+// (slower than the whole-row tile in the engine).
+// PX_TRACE builds (tools/panel_trace.py) record s_memtime per unit segment.
 #include <cstdlib>
 #include <type_traits>
 
