@@ -754,7 +754,12 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(NCH ==
 upconv_kernel(const GemmParams p) {
   static_assert(EM == E_STORE || EM == E_HEAD, "upconv epilogues");
   constexpr int NT = 512, TM = 2, TN = 2;
-  constexpr int WROWS = 9 * NCH * 32;  // weight rows of 64 B: (tap, chunk, out channel)
+  // cc > 32: the current item's chunk of the weights is restaged per item
+  // (18 KB from L2) instead of all chunks resident, so every NCH keeps the
+  // 52 KB that fit three workgroups per CU (output_conv1 at cc = 64: 72 KB,
+  // two per CU, otherwise)
+  constexpr bool SW = NCH > 1;
+  constexpr int WROWS = 9 * (SW ? 1 : NCH) * 32;  // weight rows of 64 B: (tap, chunk, out channel)
   // E_STORE stages f16 rows (store_tile_lds HALF: 2 KB per wave) in the patch
   // space, which no wave writes again before the next item's first barrier
   // bias (and the head's 1x1 weights) live in LDS: a global load in the
@@ -790,7 +795,7 @@ upconv_kernel(const GemmParams p) {
   const unsigned rowstride = (unsigned)p.cw * (unsigned)p.cc;
 
   // ---- weights, all taps and chunks, once (glds: 16 rows x 4 chunks per wave-instruction)
-  {
+  if constexpr (!SW) {
     const int lrow = lane >> 2, lch = cpch<32>(lrow, lane & 3);
     for (int q = wave; q < WROWS / 16; q += 8) {
       const int tc = q >> 1, n = (q & 1) * 16 + lrow;
@@ -894,6 +899,17 @@ upconv_kernel(const GemmParams p) {
     wait_vmc();  // this item's pass-H operands (and, first time, the weights) landed
     h_commit(vt);
     __syncthreads();  // H complete; every wave done with the previous item's MFMAs / staging
+    if constexpr (SW) {
+      // chunk c's weights (every wave has left the previous item's MFMAs),
+      // issued from asm ahead of the next item's pass-H loads and waited
+      // for by count before the second barrier
+      const int lrow = vl >> 2, lch = cpch<32>(lrow, vl & 3);
+      for (int q = wave; q < WROWS / 16; q += 8) {
+        const int n = (q & 1) * 16 + lrow;
+        glds16_asm(reinterpret_cast<const f16*>(p.W) + (size_t)n * p.ldw + (q >> 1) * p.cc + c * 32 + lch * 8,
+                   __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)(sW + q * 16 * 64)));
+      }
+    }
     // the next item's pass-H loads fly under this item's pass V, MFMAs and epilogue
     int tn = t, cn = c + 1;
     if (cn == NCH) {
@@ -928,6 +944,12 @@ upconv_kernel(const GemmParams p) {
         *reinterpret_cast<f16x8*>(sP + uoff(r, col, lc)) = v;
       }
     }
+    if constexpr (SW) {
+      // this wave's weight DMAs landed: only the next item's 2 HI pass-H
+      // loads, issued after them, may still be in flight
+      if (tn < tend) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * HI) : "memory");
+      else wait_vmc();
+    }
     __syncthreads();
     // ---- 9 taps x one 32-deep k-step of chunk c
     {
@@ -943,7 +965,7 @@ upconv_kernel(const GemmParams p) {
 #pragma unroll
         for (int j = 0; j < TN; ++j) {
           const int r = j * 16 + (lane & 15);
-          fb[j] = *reinterpret_cast<const f16x8*>(sW + ((tp * NCH + c) * 32 + r) * 64 + cpch<32>(r, lc) * 16);
+          fb[j] = *reinterpret_cast<const f16x8*>(sW + ((SW ? tp : tp * NCH + c) * 32 + r) * 64 + cpch<32>(r, lc) * 16);
         }
 #pragma unroll
         for (int i = 0; i < TM; ++i)
@@ -1068,7 +1090,7 @@ bool upconv_eligible(const GemmParams& p) {
 // that size run one tile per workgroup)
 template <int NCH>
 int upconv_grid() {
-  constexpr int lds = UPATCH + UHBUF + 9 * NCH * 32 * 64;
+  constexpr int lds = UPATCH + UHBUF + 9 * (NCH > 1 ? 1 : NCH) * 32 * 64;
   const int per_cu = 163840 / lds < 4 ? 163840 / lds : 4;
   return 256 * (per_cu > 0 ? per_cu : 1);
 }
