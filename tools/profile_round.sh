@@ -12,7 +12,7 @@ set -o pipefail
 out=$1; shift
 export TMPDIR=/tmp
 mkdir -p "$out"
-args=(--steps 5 --warmup 2 --no-b1 --no-cpu-baseline --profile-iters 1 --layers-json "$out/layers.json" "$@")
+args=(--steps 5 --warmup 2 --no-b1 --no-cpu-baseline --no-pcie --profile-iters 1 --layers-json "$out/layers.json" "$@")
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$out/stats" -o run --output-format csv -- \
   python3 bench.py "${args[@]}" > "$out/stats.log" 2>&1 || exit $?
 i=0
