@@ -1,9 +1,8 @@
+# The round-5 closing evidence session (gpurun_out/r5e7 + r5e8): GPU suite,
+# smoke, default bench + its rocprof stats and HBM traffic passes (without the
+# PCIe leg), ViT-L batch-1 bench, ViT-S batch-1 profile.
+#   /usr/local/graft/bin/gpurun --timeout 1200 -- 'bash tools/_session.sh'
 set -o pipefail
-O=gpurun_out/r5x24
+O=gpurun_out/r5e9
 mkdir -p $O
-K=--batch,48,--iters,20,--only,K384
-F=--batch,48,--iters,20,--only,fc2
-A=--no-b1,--no-cpu-baseline,--no-pcie
-bash tools/gpu_tasks.sh $O "tests:panel or test_linear or qkv_layout" kern:pon:$K env:MDE_PANEL=0 kern:poff:$K bench:poff:$A unenv:MDE_PANEL \
-  bench:pon:$A benchlib:fw4:build/var/px_fw4.so,$A kern:fbase:$F kern:fw4:$F,--lib,build/var/px_fw4.so \
-  "tests:engine_518_bench or replays or graph or lnfold or golden_518"
+bash tools/gpu_tasks.sh $O tests smoke bench:def: profile:def bench:vitl1:--encoder,vitl,--batch,1,--no-cpu-baseline,--no-pcie profile:vits1:--batch,1
