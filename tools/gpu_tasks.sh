@@ -53,7 +53,7 @@ for t in "$@"; do
       bash tools/profile_round.sh "$O/prof_$tag" "${args[@]}" || { log "profile rc=$?"; exit 1; } ;;
     pmc)
       bash tools/pmc_profile.sh "$O/pmc_$tag" -- python3 bench.py --steps 3 --warmup 1 --no-b1 --no-cpu-baseline \
-        --profile-iters 1 "${args[@]}" || { log "pmc rc=$?"; exit 1; } ;;
+        --no-pcie --profile-iters 1 "${args[@]}" || { log "pmc rc=$?"; exit 1; } ;;
     trace)
       timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --output-format csv -d "$O/trace_$tag" -o tr -- \
         python3 bench.py --no-b1 --no-cpu-baseline --profile-iters 1 "${args[@]}" > "$O/trace_$tag.log" 2>&1 \
