@@ -725,16 +725,17 @@ bool conv64p_launch(const GemmParams& p, hipStream_t st, hipError_t& err) {
 // pixels per output, and every 128-pixel workgroup restages the 9 weight
 // taps.  The bilinear upsample is separable, so this kernel builds the patch
 // in two passes over a 16 x 16 output tile (18 x 18 virtual patch):
-//   pass H: for each source row the tile touches (<= 13) and each patch
+//   pass H: for each source row the tile touches (<= 12) and each patch
 //           column, lerp the two source columns (2 loads, 1 lerp);
 //   pass V: for each patch pixel, lerp the two H rows (2 LDS reads, 1 lerp).
-// Per output pixel: ~1.7 loads and ~2.1 lerps instead of 5.6 and 4.2, and
-// the weights (all 9 taps x cc, <= 72 KB) are staged once per 256 pixels.
-// The blend is the same two-level lerp in the same order (horizontal, then
-// vertical) as conv3_kernel, so the patch is bit-identical; at cc = 32 the
-// MFMA order is too (cc > 32: 32-channel chunks, tap-major inside a chunk).
-// 8 waves x (2 tile rows x 32 channels); LDS (cc = 32) 53 KB: three
-// workgroups per CU.
+// Per output pixel: ~1.7 loads and ~2.1 lerps instead of 5.6 and 4.2.  The
+// weights: at cc = 32 all 9 taps resident (18 KB, staged once); wider, the
+// item's 32-channel chunk restaged per item.  The blend is the same
+// two-level lerp in the same order (horizontal, then vertical) as
+// conv3_kernel, so the patch is bit-identical; at cc = 32 the MFMA order is
+// too (cc > 32: 32-channel chunks, tap-major inside a chunk).  8 waves x (2
+// tile rows x 32 channels); LDS 52 KB at every cc: three workgroups per CU
+// (the patch and H buffers swizzled by column, uoff below).
 constexpr int UTH = 16, UTW = 16;                        // output tile
 constexpr int UPH = UTH + 2, UPW = UTW + 2;              // virtual patch
 // source rows per tile (host-checked, exactly): 12 keeps the cc = 32 kernel
