@@ -1414,10 +1414,20 @@ int mde_op_linear_residual(const void* a, int lda, const void* w, int ldw, int m
   OP_RET(launch_gemm(g, (hipStream_t)st), "linear_residual");
 }
 
+// E_QKV geometry: V^T stores key t at vt_pos(t), which swaps bits 2 and 3 of
+// t, so a row of tokens_pad keys holds whole 16-key groups only when
+// tokens_pad % 16 == 0 (otherwise the last group's keys land in the next row)
+static const char* qkv_geometry_error(int batch, int tokens, int heads, int tokens_pad) {
+  if (batch <= 0 || tokens <= 0 || heads <= 0) return "batch, tokens and heads must be > 0";
+  if (tokens_pad < tokens) return "tokens_pad < tokens";
+  if (tokens_pad % 16) return "tokens_pad % 16 != 0 (V^T key permutation works on 16-key groups)";
+  return nullptr;
+}
+
 int mde_op_qkv(const void* a, const void* w, int ldw, const float* bias, int batch, int tokens, int heads,
                int tokens_pad, float qscale, void* q, void* k, void* vt, void* st) {
   if (!a || !w || !bias || !q || !k || !vt) return fail(MDE_ERR_ARG, "null argument");
-  if (tokens_pad < tokens) return fail(MDE_ERR_ARG, "tokens_pad < tokens");
+  if (const char* why = qkv_geometry_error(batch, tokens, heads, tokens_pad)) return fail(MDE_ERR_ARG, why);
   GemmParams g;
   g.emode = E_QKV;
   const int D = heads * 64;
@@ -1490,7 +1500,7 @@ int mde_op_qkv_lnfold(const void* x, const float* ln_partials, float eps, const 
                       const float* c2, int batch, int tokens, int heads, int tokens_pad, float qscale, void* q, void* k,
                       void* vt, void* st) {
   if (!x || !ln_partials || !wg || !c1 || !c2 || !q || !k || !vt) return fail(MDE_ERR_ARG, "null argument");
-  if (tokens_pad < tokens) return fail(MDE_ERR_ARG, "tokens_pad < tokens");
+  if (const char* why = qkv_geometry_error(batch, tokens, heads, tokens_pad)) return fail(MDE_ERR_ARG, why);
   GemmParams g;
   g.emode = E_QKV;
   const int D = heads * 64;

@@ -517,7 +517,7 @@ bool panel_gemm_eligible(const GemmParams& p) {
     return knob(KNOB_PANEL) == 2 && p.xh && p.ls && !p.lnst_in && !(p.ldo & 3) && !((uintptr_t)p.xh & 7) && p.ldo >= p.N && !p.partial &&
            (!p.lnst_out || (p.lnst_ns * 32 == p.N && p.lnst_rows >= p.M));
   if (p.emode == E_QKV)
-    return p.heads > 0 && p.heads * 64 * 3 == p.N && p.T > 0 && p.Tpad >= p.T && p.q && p.k && p.vt &&
+    return p.heads > 0 && p.heads * 64 * 3 == p.N && p.T > 0 && p.Tpad >= p.T && !(p.Tpad & 15) && p.q && p.k && p.vt &&
            !((uintptr_t)p.q & 7) && !((uintptr_t)p.k & 7) && p.act == ACT_NONE;
   return false;
 }

@@ -138,3 +138,17 @@ def test_two_hip_runtimes_are_refused(lib_path):
                       "    print('REFUSED', e)\n")
     assert rc == 0, out
     assert "REFUSED two HIP runtimes" in out, out
+
+
+@pytest.mark.parametrize("tpad, heads, msg", [(40, 6, b"% 16"), (36, 6, b"tokens_pad < tokens"), (48, 0, b"> 0")])
+def test_qkv_ops_reject_bad_geometry(lib_path, tpad, heads, msg):
+    """V^T stores key t at vt_pos(t) (bits 2 and 3 swapped), so a
+    tokens_pad that is not a multiple of 16 would spill the last key group into
+    the next row.  Both qkv entry points refuse it before touching the device."""
+    from monocular_depth_estimation_trt_amd import _lib
+    lib = _lib.lib()
+    p = 4096  # never dereferenced: the geometry check runs first
+    rc = lib.mde_op_qkv(p, p, 384, p, 1, 37, heads, tpad, 0.125, p, p, p, None)
+    assert rc != 0 and msg in lib.mde_last_error()
+    rc = lib.mde_op_qkv_lnfold(p, p, 1e-6, p, 384, p, p, 1, 37, heads, tpad, 0.125, p, p, p, None)
+    assert rc != 0 and msg in lib.mde_last_error()
