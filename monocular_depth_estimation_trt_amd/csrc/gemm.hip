@@ -53,6 +53,15 @@
 #define MDE_GEMM_STAGES 2  // LDS ring depth for dense A (>2: counted-vmcnt pipeline)
 #endif
 
+// Phase-isolation hooks (MDE_EXP_NOLOOP / NOLOAD / NOMFMA / NOEPI) compile
+// parts of the GEMM out and produce WRONG outputs: tools/ablate.py builds them
+// as separate variant libraries only, with MDE_EXPERIMENT defined as well;
+// _build.build_library never passes defines to the in-tree libmde_hip.so.
+#if (defined(MDE_EXP_NOLOOP) || defined(MDE_EXP_NOLOAD) || defined(MDE_EXP_NOMFMA) || defined(MDE_EXP_NOEPI)) && \
+    !defined(MDE_EXPERIMENT)
+#error "MDE_EXP_* hooks need -DMDE_EXPERIMENT (variant libraries only, never the product build)"
+#endif
+
 namespace mde {
 
 namespace {

@@ -38,6 +38,7 @@
 // "panel" = 2: at N = 384 a panel has 6 units and its load is not amortised
 // (slower than the whole-row tile in the engine).
 // PX_TRACE builds (tools/panel_trace.py) record s_memtime per unit segment.
+#include <atomic>
 #include <cstdlib>
 #include <type_traits>
 
@@ -480,16 +481,22 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
 
 }  // namespace
 
+// CUs of the current device, cached per device id (persistent grids size
+// themselves by it; hipGetDevice is per host thread, so each thread asks
+// about the device it launches on)
 int cu_count() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0, v = 0;
-    if (hipGetDevice(&dev) == hipSuccess && hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
-      n = v;
-    else
-      n = 256;
+  constexpr int kMaxDev = 64;
+  static std::atomic<int> cache[kMaxDev];  // 0 = not queried yet
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0) return 256;
+  if (dev < kMaxDev) {
+    const int c = cache[dev].load(std::memory_order_relaxed);
+    if (c > 0) return c;
   }
-  return n;
+  int v = 0;
+  if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0) v = 256;
+  if (dev < kMaxDev) cache[dev].store(v, std::memory_order_relaxed);  // racing threads store the same value
+  return v;
 }
 
 #ifdef PX_TRACE

@@ -57,10 +57,16 @@ def test_product_has_no_unclear_dma_address_reuse():
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
     import dma_hazard_scan as S
     findings, cleared = [], []
+    dma_sites = 0
     for obj in S.product_objects():
-        f, c = S.classify(S.scan(S.disassemble(obj)))
+        text = S.disassemble(obj)
+        dma_sites += text.count("global_load_lds")
+        f, c = S.classify(S.scan(text))
         findings += f
         cleared += c
+    # the scan saw the product's LDS-DMA code at all (an empty disassembly
+    # would otherwise pass vacuously)
+    assert dma_sites > 100, dma_sites
     assert not findings, findings[:5]
     assert all(S.dma_form(h[1]) == "vaddr64" for h in cleared), [h for h in cleared if S.dma_form(h[1]) != "vaddr64"][:5]
 

@@ -137,7 +137,9 @@ def disassemble(obj: str) -> str:
         subprocess.run([OBJDUMP, "--offloading", c], capture_output=True, check=True)
         dev = [f for f in glob.glob(c + ".*") if f.endswith("gfx950")]
         if not dev:
-            return ""
+            # a silent "" would let a caller scan nothing and report clean
+            # (e.g. after an MDE_OFFLOAD_ARCH or llvm-objdump naming change)
+            raise RuntimeError(f"{obj}: no gfx950 device bundle found by {OBJDUMP} --offloading")
         return subprocess.run([OBJDUMP, "-d", dev[0]], capture_output=True, text=True, check=True).stdout
     finally:
         shutil.rmtree(d)
