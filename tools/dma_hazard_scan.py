@@ -128,14 +128,17 @@ def classify(hits):
     return findings, cleared
 
 
-def disassemble(obj: str) -> str:
-    """Device (gfx950) disassembly of a hipcc object or shared library."""
+def disassemble(obj: str, require: bool = True) -> str:
+    """Device (gfx950) disassembly of a hipcc object or shared library;
+    `require=False` for objects that may hold host code only (engine.hip)."""
     d = tempfile.mkdtemp()
     try:
         c = os.path.join(d, os.path.basename(obj))
         shutil.copy(obj, c)
         subprocess.run([OBJDUMP, "--offloading", c], capture_output=True, check=True)
         dev = [f for f in glob.glob(c + ".*") if f.endswith("gfx950")]
+        if not dev and not require:
+            return ""
         if not dev:
             # a silent "" would let a caller scan nothing and report clean
             # (e.g. after an MDE_OFFLOAD_ARCH or llvm-objdump naming change)
@@ -156,9 +159,10 @@ def main(argv: list[str]) -> int:
     files = [a for a in argv if not a.startswith("--")]
     if "--product" in argv:
         files += product_objects()
-    total_f = total_c = 0
+    total_f = total_c = dma = 0
     for f in files:
-        text = open(f).read() if f.endswith(".s") else disassemble(f)
+        text = open(f).read() if f.endswith(".s") else disassemble(f, require="--product" not in argv)
+        dma += text.count("global_load_lds") + text.count(" lds\n")
         findings, cleared = classify(scan(text))
         total_f += len(findings)
         total_c += len(cleared)
@@ -168,7 +172,10 @@ def main(argv: list[str]) -> int:
         for k in sorted({h[0] for h in show})[:40]:
             ex = next(h for h in show if h[0] == k)
             print(f"   {k[:90]}\n      {ex[1]}\n      -> {ex[2]}")
-    print(f"total: {total_f} finding(s), {total_c} cleared site(s)")
+    print(f"total: {total_f} finding(s), {total_c} cleared site(s), {dma} LDS-DMA instruction(s) scanned")
+    if files and not dma:
+        print("error: no LDS-DMA instruction in the scanned device code (nothing was checked)")
+        return 2
     return 1 if total_f else 0
 
 
