@@ -56,10 +56,18 @@ constexpr int PKSEG = PK / 64;       // 128-B LDS row segments of a W row (6)
 constexpr int PBN = 64;              // output columns per unit = W rows per chunk
 constexpr int PBM = 256;             // panel rows: 8 waves x 32
 constexpr int PCHB = PBN * PK * 2;   // one W chunk in LDS: 48 KB
-constexpr int PSLOTS = 2;            // W ring depth
+#ifndef PX_SLOTS
+#define PX_SLOTS 3
+#endif
+constexpr int PSLOTS = PX_SLOTS;     // W ring depth: chunk j + PSLOTS - 1 issued at the top of unit j
+constexpr int PLEAD = PSLOTS - 1;    // units between a chunk's issue and its use
 constexpr int PNMAX = 1536;          // widest N (bias / lnc1 table)
 constexpr int PTAB = PSLOTS * PCHB;  // bias / lnc1 table offset
-constexpr int PLDS = PTAB + 2 * PNMAX * 4;  // 108 KB
+constexpr int PLDS = PTAB + 2 * PNMAX * 4;  // 156 KB at 3 slots (108 KB at 2)
+static_assert(PLDS <= 163840, "LDS");
+#ifndef PX_PACKED
+#define PX_PACKED 1  // 1: the epilogue's fp32 arithmetic on packed f32 pairs (v_pk_*_f32)
+#endif
 #ifndef PEPI_STRIDE
 #define PEPI_STRIDE 1  // k-substeps between the epilogue's block pairs
 #endif
@@ -99,6 +107,12 @@ MDE_DEV void pglds_chunk(const char* base, unsigned off, unsigned lds) {
 // just before, that drained the ring each unit).  gfx9 simm16: vmcnt [3:0] +
 // [15:14] = 0, expcnt [6:4] = 7, lgkmcnt [11:8] = 15
 MDE_DEV void pwait_vm0() { __builtin_amdgcn_s_waitcnt(0x0F70); }
+// s_waitcnt vmcnt(N) (N < 64; expcnt / lgkmcnt not waited), the same way
+template <int N>
+MDE_DEV void pwait_vm() {
+  static_assert(N >= 0 && N < 64, "vmcnt");
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | 0x0F70);
+}
 
 // raw workgroup barrier: LDS-DMA stays in flight (__syncthreads would drain vmcnt)
 MDE_DEV void pbarrier() {
@@ -114,11 +128,16 @@ __device__ __attribute__((aligned(16))) f16x4 g_psink[64];
 #ifdef PX_TRACE
 // timing build only (tools/panel_trace.py): per (block < 8, wave, unit <
 // 96) the s_memtime after the unit's barrier and before its end-of-unit wait
-__device__ unsigned long long g_ptrace[8][8][96][3];
+// (slot 3: s_memrealtime, 100 MHz, at the unit start -- the clock check)
+__device__ unsigned long long g_ptrace[8][8][96][4];
 #define PTRACE(SG, K)                                                     \
   if (blockIdx.x < 8 && (SG) >= 0 && (SG) < 96) {                         \
     const unsigned long long tt = __builtin_amdgcn_s_memtime();           \
     if (lane == 0) g_ptrace[blockIdx.x][wave][(SG)][(K)] = tt;            \
+    if ((K) == 0) {                                                       \
+      const unsigned long long rt = __builtin_amdgcn_s_memrealtime();     \
+      if (lane == 0) g_ptrace[blockIdx.x][wave][(SG)][3] = rt;            \
+    }                                                                     \
   }
 #else
 #define PTRACE(SG, K)
@@ -133,9 +152,27 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int l15 = lane & 15, hq = lane >> 4;
-  const int U = nch * npan;
-  const int u0 = (int)((long long)blockIdx.x * U / gridDim.x);
-  const int nu = (int)((long long)(blockIdx.x + 1) * U / gridDim.x) - u0;
+  // the workgroup's units (panel-major (panel, chunk) pairs): q = npan / G
+  // whole panels first -- each panel's A is loaded by one workgroup, once --
+  // then the leftover panels' units spread evenly over all workgroups as a
+  // tail (at B = 48: 257 panels, 256 workgroups -> 24 units each plus one
+  // tail unit for 24 of them).  npan < G: all units are tail (an even split).
+  const int G = gridDim.x, g = blockIdx.x;
+#ifndef PX_PART
+// 1: whole panels per workgroup + an even tail (A read once: qkv 295 -> ~205
+// MB, fc1 341 -> ~255 MB per B = 48 launch); 0 (default): every workgroup an
+// even contiguous share of all units, two panels for most.  Measured in the
+// graph (round 6, same box): the whole-panel form made the NEXT kernels
+// slower (the 256 x 128 residual GEMMs +40 us, attention +15 us per forward)
+// by more than it saved, step 5724 (0) vs 5685 (1) img/s
+#define PX_PART 0
+#endif
+  const int q = PX_PART ? npan / G : 0;
+  const int m0 = g * q * nch, nm = q * nch;
+  const int tb = q * G * nch, T = nch * npan - tb;
+  const int t0 = tb + (int)((long long)g * T / G);
+  const int nu = nm + tb + (int)((long long)(g + 1) * T / G) - t0;
+  auto gunit = [&](int j) __attribute__((always_inline)) { return j < nm ? m0 + j : t0 + (j - nm); };
 
   // per-column bias and folded-LN column sums, read by every epilogue
   // (E_RESID: tab_c holds the layer scale instead)
@@ -151,10 +188,11 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
   const unsigned woff = (unsigned)((drow * p.ldw + (((lane & 7) ^ drow) * 8)) * 2);  // bytes
   static_assert(PKSEG == 6 && PBN == 64, "pglds_chunk: 6 row segments of 64 rows");
   const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)smem) + wave * 1024;
-  auto issue = [&](int rel) __attribute__((always_inline)) {  // unit u0 + rel -> slot rel & 1
-    const int c = (u0 + rel) % nch;
+  auto issue = [&](int rel) __attribute__((always_inline)) {  // local unit rel -> slot rel % PSLOTS
+    // (wave-uniform operands made explicitly scalar: the asm takes SGPRs)
+    const int c = __builtin_amdgcn_readfirstlane(gunit(rel) % nch);
     pglds_chunk(reinterpret_cast<const char*>(p.W) + (size_t)(c * PBN + 8 * wave) * p.ldw * 2, woff,
-                lds0 + (rel & 1) * PCHB);
+                __builtin_amdgcn_readfirstlane(lds0 + (rel % PSLOTS) * PCHB));
   };
 
   // ---- A: this wave's 32 panel rows as MFMA B-operand fragments ----
@@ -327,7 +365,34 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
       x[2 * e + 1] = f32x2{v[2], v[3]};
     }
     f32x2 y[4];
-    if constexpr (ACT == ACT_GELU) {
+    if constexpr (ACT == ACT_GELU && !PX_PACKED) {
+      // gelu_erf per value, the 8 values' chains in lockstep: the fused
+      // operations of gelu_erf2 in the same order on scalar registers (packed
+      // f32 VALU beside MFMAs costs more issue time than the two scalar ops,
+      // MI355X_MICROARCH.md cycle constants)
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {  // one block's 4 values per pass (8 chains spill the fold kernels)
+        float xv[4], xc[4], x2[4], t[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xv[i] = x[2 * e + (i >> 1)][i & 1];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) xc[i] = __builtin_amdgcn_fmed3f(xv[i], -8.f, 8.f);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) x2[i] = __fmul_rn(xc[i], xc[i]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t[i] = fmaf(0.001014263055f, x2[i], -0.106775724f);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t[i] = fmaf(t[i], x2[i], -2.301121339f);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t[i] = __fmul_rn(xc[i], t[i]);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t[i] = __fadd_rn(1.f, __builtin_amdgcn_exp2f(t[i]));
+#pragma unroll
+        for (int i = 0; i < 4; ++i) t[i] = __builtin_amdgcn_rcpf(t[i]);
+        y[2 * e] = f32x2{__fmul_rn(xv[0], t[0]), __fmul_rn(xv[1], t[1])};
+        y[2 * e + 1] = f32x2{__fmul_rn(xv[2], t[2]), __fmul_rn(xv[3], t[3])};
+      }
+    } else if constexpr (ACT == ACT_GELU) {
       const f32x2 cc = {0.001014263055f, 0.001014263055f}, cb2 = {-0.106775724f, -0.106775724f},
                   ca = {-2.301121339f, -2.301121339f};
       f32x2 xc[4], x2[4], t[4], d[4];
@@ -372,10 +437,10 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
   // hoisting all 48 fragment reads (192 VGPRs) and keeps each epilogue block
   // beside its substep's 8 MFMAs.
   const int cx = (hq ^ (lane & 7)) << 4;  // physical chunk of logical chunk hq in rows r (r & 7 = lane & 7)
-  auto unit = [&](auto off_tag, int j, f32x4(&accC)[2][4], const f32x4(&accP)[2][4], bool epi, int ppnl, int pc,
+  auto unit = [&](auto off_tag, int slot, f32x4(&accC)[2][4], const f32x4(&accP)[2][4], bool epi, int ppnl, int pc,
                   const float (&pmean)[2], const float (&prstd)[2], int cpnl, int cc) __attribute__((always_inline)) {
     constexpr int OFF = decltype(off_tag)::value;
-    const char* sw = smem + (j & 1) * PCHB + l15 * 128;
+    const char* sw = smem + slot * PCHB + l15 * 128;
 #pragma unroll
     for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
@@ -419,8 +484,20 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
     }
   };
 
-  // ---- prologue: chunk 0 in flight ----
-  issue(0);
+#ifndef PX_PRIO
+#define PX_PRIO 1
+#endif
+#if PX_PRIO
+  // static priority for the second-dispatched half (MI355X_MICROARCH.md
+  // "Two waves per SIMD" item 4): in-kernel trace, the lagging half's work
+  // per unit 7026 -> 4301 ticks (the other half's 5005 -> 7026), graph fc1
+  // 1.48 -> 1.45 ms per B = 48 forward
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
+  // ---- prologue: chunks 0 .. PLEAD - 1 in flight ----
+#pragma unroll
+  for (int r = 0; r < PLEAD; ++r)
+    if (r < nu) issue(r);
   // ---- the unit loop, one copy per epilogue placement: the two waves of a
   // SIMD (w, w + 4) run their epilogue VALU in different k-substeps, so one's
   // VALU-heavy substeps meet the other's MFMA-only ones (the same substeps
@@ -429,7 +506,7 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
   // per-unit branch between two unit bodies merged both accumulator sets at
   // every join and spilled.  Both copies run the same barrier sequence.
   auto run = [&](auto off_tag) __attribute__((always_inline)) {
-    f32x4 acc0[2][4], acc1[2][4];  // this unit's / the previous unit's accumulators
+    f32x4 acc0[2][4], acc1[2][4];  // the two accumulator sets: a unit's MFMAs / the previous unit's epilogue
 #pragma unroll
     for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
@@ -437,43 +514,62 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
     float lmean[2] = {0.f, 0.f}, lrstd[2] = {1.f, 1.f};  // this panel's LN stats
     int ppnl = 0, pc = 0;                                 // panel and chunk of the unit whose epilogue runs next
     // outer loop: one run of units per A panel (af loop-invariant inside)
-    auto epi_all = [&]() __attribute__((always_inline)) {  // a unit's whole epilogue, standalone
+    auto epi_all = [&](const f32x4(&accP)[2][4]) __attribute__((always_inline)) {  // a unit's whole epilogue, standalone
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const ColB cb[2] = {col_read(pc, (2 * q) & 3), col_read(pc, (2 * q + 1) & 3)};
-        epi_pair(2 * q, ppnl, pc, acc1, lmean, lrstd, cb, true);
+        epi_pair(2 * q, ppnl, pc, accP, lmean, lrstd, cb, true);
       }
     };
     int j = 0;
     while (j < nu) {
-      const int pnl = (u0 + j) / nch;
-      const int jend = min(nu, (pnl + 1) * nch - u0);
+      const int gu = gunit(j), pnl = gu / nch;
+      // the run: this panel's units inside the current (main or tail) range
+      const int jend = min(j < nm ? nm : nu, j + (pnl + 1) * nch - gu);
       // the previous panel's last epilogue runs here, on its own (once per
       // panel switch): the stats registers then hold one panel at a time
-      if (j > 0) epi_all();
+      if (j > 0) epi_all(acc1);
       load_panel(pnl);
       if constexpr (FOLD) panel_stats(pnl, lmean, lrstd);
-      pwait_vm0();  // A and chunk j landed (once per panel)
-      for (int j0 = j; j < jend; ++j) {
-        pbarrier();  // chunk j visible to all waves; slot (j + 1) & 1 (unit j - 1) fully read
-        PTRACE(j, 0)
-        if (j + 1 < nu) issue(j + 1);
-        // fixed accumulator roles and a copy per unit (32 moves per 96
-        // MFMAs): alternating the two sets by unit parity left both live
-        // across a branch and spilled
-        unit(off_tag, j, acc0, acc1, j > j0, pnl, pc, lmean, lrstd, pnl, (u0 + j) - pnl * nch);
+      pwait_vm0();  // A and every issued chunk landed (once per panel)
+      const int j0 = j;
+      // one unit: chunk jj visible to all waves after the barrier, and slot
+      // (jj + PLEAD) % PSLOTS (unit jj - 1's) read by all, so chunk jj + PLEAD
+      // goes into it.  At the end, chunk jj + 1 must have landed: it was issued
+      // at the top of unit jj + 1 - PLEAD, and every unit since issued at least
+      // 8 vector-memory ops after it (the epilogue's stores; E_QKV's V^T
+      // chunks 32), so vmcnt(8 PLEAD) waits for it and leaves the newer chunk
+      // DMAs and this unit's stores in flight (an older store waited for too
+      // is long done)
+      auto step = [&](int jj, f32x4(&accC)[2][4], const f32x4(&accP)[2][4]) __attribute__((always_inline)) {
+        pbarrier();
+        PTRACE(jj, 0)
+        if (jj + PLEAD < nu) issue(jj + PLEAD);
+        const int cc = gunit(jj) - pnl * nch;
+        unit(off_tag, jj % PSLOTS, accC, accP, jj > j0, pnl, pc, lmean, lrstd, pnl, cc);
+        ppnl = pnl;
+        pc = cc;
+        PTRACE(jj, 1)
+        if constexpr (EM == E_RESID) pwait_vm0();  // (its residual loads: consumed next unit)
+        else pwait_vm<8 * PLEAD>();
+        PTRACE(jj, 2)
+      };
+      // two units per iteration with the accumulator roles swapped: no copy
+      // of the 32 accumulator registers per unit
+      for (; j + 1 < jend; j += 2) {
+        step(j, acc0, acc1);
+        step(j + 1, acc1, acc0);
+      }
+      if (j < jend) {
+        step(j, acc0, acc1);
 #pragma unroll
         for (int ib = 0; ib < 2; ++ib)
 #pragma unroll
           for (int jb = 0; jb < 4; ++jb) acc1[ib][jb] = acc0[ib][jb];
-        ppnl = pnl;
-        pc = (u0 + j) - pnl * nch;
-        PTRACE(j, 1)
-        pwait_vm0();  // chunk j + 1 landed; this unit's stores done
-        PTRACE(j, 2)
+        ++j;
       }
     }
-    epi_all();  // the last unit's epilogue
+    epi_all(acc1);  // the last unit's epilogue
   };
   if (wave < 4) run(std::integral_constant<int, 0>{});
   else run(std::integral_constant<int, PEPI_OFF1>{});

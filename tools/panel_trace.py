@@ -39,7 +39,7 @@ def main():
     for _ in range(3):
         L.mde_op_linear(ptr(x), k, ptr(wp), wp.shape[1], m, n, k, ptr(b), a.act, ptr(out), n, stream())
     torch.cuda.synchronize()
-    buf = np.zeros((8, 8, 96, 3), dtype=np.uint64)
+    buf = np.zeros((8, 8, 96, 4), dtype=np.uint64)
     fn = getattr(L, "mde_debug_panel_trace")
     fn.argtypes = [C.c_void_p]
     assert fn(buf.ctypes.data) == 0
@@ -59,6 +59,21 @@ def main():
     r = np.array(rows, dtype=np.float64)
     print(f"unit (s_memtime ticks, n={len(r)}): length {r[:, 0].mean():7.0f}  work {r[:, 1].mean():7.0f}  "
           f"vmcnt wait {r[:, 2].mean():7.0f}  barrier {r[:, 3].mean():7.0f}  work spread over waves {r[:, 4].mean():7.0f}")
+
+    # in-kernel clock: memtime ticks per 100 MHz realtime tick over each wave's units
+    ck = []
+    for blk in range(8):
+        for w in range(8):
+            mt, rt = t[blk, w, :nseg, 0], t[blk, w, :nseg, 3]
+            if rt[-1] > rt[0]:
+                ck.append((mt[-1] - mt[0]) / (rt[-1] - rt[0]) * 0.1)
+    if ck:
+        print(f"in-kernel clock {np.median(ck):.3f} GHz (median over waves); units {nseg}, "
+              f"first -> last unit start {np.median([(t[b, 0, nseg - 1, 3] - t[b, 0, 0, 3]) / 100.0 for b in range(8)]):.1f} us")
+    lo = np.array([(t[b, :4, 1:nseg - 1, 1] - t[b, :4, 1:nseg - 1, 0]).mean() for b in range(8)])
+    hi = np.array([(t[b, 4:, 1:nseg - 1, 1] - t[b, 4:, 1:nseg - 1, 0]).mean() for b in range(8)])
+    print(f"work per unit: waves 0-3 {lo.mean():7.0f}  waves 4-7 {hi.mean():7.0f}")
+
 
 if __name__ == "__main__":
     main()
