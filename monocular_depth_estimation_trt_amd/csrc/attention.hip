@@ -159,6 +159,11 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
   const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = NS > 1 ? wave_all / NWQ : 0;   // key group
   const int wave = wave_all - grp * NWQ;         // query wave within the group
+  // static priority for the second-dispatched half of the 8-wave workgroup
+  // (MI355X_MICROARCH.md "Two waves per SIMD" item 4): round 6, B = 48 graph
+  // step +0.5-0.6 % in two same-box pairs (5730 -> 5758 / 5767 img/s,
+  // gpurun_out r6s7; round 3 had measured no gain on the older kernel)
+  if (NW == 8 && NS == 1 && wave_all >= 4) __builtin_amdgcn_s_setprio(1);
   // XCD-aware block order: workgroups are dealt round-robin over the 8 XCDs
   // (linear id % 8 shares an L2); remap so each XCD takes a contiguous run
   // of (head, query block) pairs and a head's K/V^T is fetched into one L2,

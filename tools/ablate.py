@@ -64,10 +64,6 @@ VARIANTS = {
 }""", 1)]),
     # candidate (not an ablation): static priority for the second-dispatched
     # half of an 8-wave workgroup (MI355X_MICROARCH.md "Two waves per SIMD" 4)
-    "attn_prio": ("attention.hip", [
-        ("""  const int wave = wave_all - grp * NWQ;         // query wave within the group""",
-         """  const int wave = wave_all - grp * NWQ;         // query wave within the group
-  if (NW == 8 && NS == 1 && wave_all >= 4) __builtin_amdgcn_s_setprio(1);""", 1)]),
     # candidate (not an ablation): batch-1 stores / qkv whose 128^2 grid
     # overhangs the CUs by a partial round (ViT-L B=1 qkv 264, fc1 352 tiles)
     # on 256 x 128 tiles (8 waves of 64 x 64, BK 32 x 3 stages, two per CU):
