@@ -62,8 +62,6 @@ VARIANTS = {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }""", """MDE_DEV void wait_vm_n() {
 }""", 1)]),
-    # candidate (not an ablation): static priority for the second-dispatched
-    # half of an 8-wave workgroup (MI355X_MICROARCH.md "Two waves per SIMD" 4)
     # candidate (not an ablation): batch-1 stores / qkv whose 128^2 grid
     # overhangs the CUs by a partial round (ViT-L B=1 qkv 264, fc1 352 tiles)
     # on 256 x 128 tiles (8 waves of 64 x 64, BK 32 x 3 stages, two per CU):
