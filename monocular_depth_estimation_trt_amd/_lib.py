@@ -247,7 +247,9 @@ def call(name: str, *args) -> None:
         raise MDEError(name, rc, last_error())
 
 
-TUNING = ("splitk", "lnfold", "conv_narrow", "upconv", "gemm256", "deep64", "w8small", "conv_persist", "panel")
+TUNING = ("splitk", "lnfold", "conv_narrow", "upconv", "gemm256", "deep64", "w8small", "conv_persist", "panel",
+          "panel32", "narrow_resid")
+TUNING_DEFAULT = {"panel32": 0}  # the library's defaults where not 1 (tuning.hip kKnobs)
 
 
 def get_tuning(name: str) -> int:

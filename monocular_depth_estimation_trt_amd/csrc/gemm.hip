@@ -515,6 +515,20 @@ bool deep64(long long wgs) { return knob(KNOB_DEEP64) && wgs <= 512; }
 // Switch "w8small".
 bool w8small(long long wgs) { return knob(KNOB_W8SMALL) && wgs < 512; }
 
+// Residual updates whose 64^2 grid is under one workgroup per CU (ViT-S
+// batch 1: fc2 K 1536 and proj K 384 at 1370 x 384, 132 tiles) on 32 x 64
+// tiles (258 workgroups, the whole K loop, 4-deep ring): no split-K slices
+// and no reduce launch for fc2 (round 5 measured ViT-S B = 1 0.792 -> 0.765
+// ms per forward, profiles/r05_b1_resid_narrow.txt; not bit-identical to the
+// split path -- one K loop instead of three slices added in order).  Switch
+// "narrow_resid".
+bool narrow_resid(const GemmParams& p) {
+  if (!knob(KNOB_NARROW_RESID) || p.amode != A_DENSE || p.emode != E_RESID) return false;
+  const long long t64 = (long long)((p.M + 63) / 64) * ((p.N + 63) / 64);
+  const long long t32 = (long long)((p.M + 31) / 32) * ((p.N + 63) / 64);
+  return t64 < 256 && t32 >= 192 && t32 <= 512;
+}
+
 template <int AM, int EM>
 hipError_t dispatch(const GemmParams& p, hipStream_t st) {
   if constexpr (EM == E_HEAD) {
@@ -542,6 +556,7 @@ hipError_t dispatch(const GemmParams& p, hipStream_t st) {
       // 0.427/0.431 -> 0.419/0.425 ms per forward, two same-box runs; fc2 at
       // K 1536 loses, 0.86 -> 0.97)
       if (p.K <= 384 && big >= kBigTileMin) return run<128, 64, 4, 1, AM, EM>(p, st);
+      if (narrow_resid(p)) return run<32, 64, 2, 2, AM, EM, 64, 4>(p, st);
     }
     if (big >= kBigTileMin) {
       // short-K stores (ViT-S/B qkv, fc1: K 384 / 768 -> 6-12 K-steps, the
@@ -688,7 +703,7 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
   if (p.amode != A_DENSE && conv_direct_supported(p) && !prefer_im2col(p))
     return launch_conv3(p, st);
   if ((p.emode == E_RESID || p.emode == E_PATCH) && p.xh && ((uintptr_t)p.xh & 15)) return hipErrorInvalidValue;
-  if (p.emode == E_RESID && p.splitk > 1 && p.partial && p.amode == A_DENSE) {
+  if (p.emode == E_RESID && p.splitk > 1 && p.partial && p.amode == A_DENSE && !narrow_resid(p)) {
     // small M, long K (B = 1 fc2: 132 64^2 tiles x 24 K-steps): S slices of
     // the K loop fill the chip, a second kernel adds them in slice order.
     // When 128^2 tiles x 4 slices still give >= 320 workgroups (ViT-L /

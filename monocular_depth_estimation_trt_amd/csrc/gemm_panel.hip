@@ -124,6 +124,7 @@ MDE_DEV void pbarrier() {
 // target of the stores of rows >= M (keeps the epilogue branch-free, so it
 // stays in the MFMA stream's basic block)
 __device__ __attribute__((aligned(16))) f16x4 g_psink[64];
+__device__ __attribute__((aligned(16))) uint4 g_psink8[64];  // (panel32's 16-B stores)
 
 #ifdef PX_TRACE
 // timing build only (tools/panel_trace.py): per (block < 8, wave, unit <
@@ -575,6 +576,323 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
   else run(std::integral_constant<int, PEPI_OFF1>{});
 }
 
+
+// ---------------------------------------------------------------------------
+// panel32_kernel (switch "panel32"): the same A-stationary panels, W ring and
+// unit loop as panel_gemm_kernel, with
+//  * v_mfma_f32_32x32x16_f16: a unit is 2 x 24 MFMAs per wave instead of
+//    96 of 16x16x32 -- an MFMA holds the SIMD's vector issue for 8 cycles
+//    whatever its size (MI355X_MICROARCH.md cycle constants), so the issue
+//    slots the MFMAs take halve, and they are what the epilogue's VALU
+//    competes for (in-kernel trace: the two waves of a SIMD share one issue
+//    port and the unit length is their summed issue time);
+//  * the folded LayerNorm's mean term as the accumulator's INITIAL value,
+//    acc0 = -mean * c1 (per row x per column), so the epilogue is
+//    y = rstd * acc + c2 (one fma) instead of rstd * acc - rstd * mean * c1 + c2
+//    (mul, fma, add).  Not bit-identical to the 128^2 kernel (other fp32
+//    association): tests/test_gpu_ops.py::test_panel32_matches_tile_kernel
+//    bounds the difference by the f16 output rounding.
+// Measured (round 6, B = 48, same box): per layer qkv 1.22 -> 1.12-1.17 ms,
+// fc1 1.55-1.59 -> 1.53-1.57 ms per forward, but the graph step unchanged
+// within its +-1 % noise over five pairs, and the in-graph clock of the last
+// fc1 (tools/graph_clock.py, s_memtime / s_memrealtime) 1.91 GHz against 2.02
+// for panel_gemm_kernel: fewer ticks per unit (7622 vs 7751) at a lower clock
+// (the denser body draws more power -- MI355X_MICROARCH.md DVFS item 4), 3.98
+// vs 3.84 us per unit.  Off by default (switch "panel32").  A two-workgroups-
+// per-CU form (4 waves each, separate barrier domains) measured slower still
+// (fc1 1.68 ms per forward) and was removed.
+// W LDS image: 6 segments of 64 rows x 128 B, logical 16-B chunk lc of row r
+// at physical chunk lc ^ ((r >> 1) & 7): the 32-row x 2-chunk operand reads
+// are conflict-free in every ds_read_b128 lane group.
+// Lane layout (32x32x16): W fragment = 32 output columns x 16 k (row l & 31,
+// k 8 (l >> 5) .. +7); A fragment = the wave's 32 rows x 16 k (row l & 31);
+// the accumulator of n-block nb holds row l & 31, columns nb * 32 + 8 g +
+// 4 (l >> 5) + i in register 4 g + i.
+constexpr int P3KS = PK / 16;  // 32x32x16 k-steps per unit (24)
+#ifndef P3_OFF1
+#define P3_OFF1 12  // first epilogue k-step of waves 4-7 (waves 0-3: 0)
+#endif
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+MDE_DEV f32x16 pmfma32(const f16x8& a, const f16x8& b, const f32x16& c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+template <int EM, int ACT, bool FOLD>
+__global__ void __launch_bounds__(512) panel32_kernel(const GemmParams p, int nch, int npan) {
+  static_assert(EM == E_STORE || EM == E_QKV, "panel32: E_STORE / E_QKV");
+  __shared__ __attribute__((aligned(16))) char smem[PLDS];
+  float* tab_b = reinterpret_cast<float*>(smem + PTAB);
+  float* tab_c = tab_b + PNMAX;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int l31 = lane & 31, hh = lane >> 5;
+  // units: an even contiguous share of the (panel, chunk) pairs
+  const int U = nch * npan;
+  const int u0 = (int)((long long)blockIdx.x * U / gridDim.x);
+  const int nu = (int)((long long)(blockIdx.x + 1) * U / gridDim.x) - u0;
+
+  for (int i = tid; i < p.N; i += 512) {
+    tab_b[i] = p.bias ? p.bias[i] : 0.f;
+    tab_c[i] = FOLD ? p.lnc1[i] : 0.f;
+  }
+
+  // ---- W chunk DMA: wave w fills rows 8w .. 8w + 7 of each 128-B row
+  // segment; lane -> (row 8w + (lane >> 3), physical chunk lane & 7) fetches
+  // logical chunk (lane & 7) ^ ((row >> 1) & 7)
+  const int drow = lane >> 3;
+  const unsigned woff =
+      (unsigned)((drow * p.ldw + (((lane & 7) ^ (((8 * wave + drow) >> 1) & 7)) * 8)) * 2);
+  const unsigned lds0 = __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)smem) + wave * 1024;
+  auto issue = [&](int rel) __attribute__((always_inline)) {
+    const int c = __builtin_amdgcn_readfirstlane((u0 + rel) % nch);
+    pglds_chunk(reinterpret_cast<const char*>(p.W) + (size_t)(c * PBN + 8 * wave) * p.ldw * 2, woff,
+                __builtin_amdgcn_readfirstlane(lds0 + (rel % PSLOTS) * PCHB));
+  };
+
+  // ---- A: the wave's 32 panel rows, k-step s = k 16 s + 8 hh .. +7
+  f16x8 af[P3KS];
+  auto row_of = [&](int pnl) __attribute__((always_inline)) { return pnl * PBM + wave * 32 + l31; };
+  auto load_panel = [&](int pnl) __attribute__((always_inline)) {
+    const int m = row_of(pnl);
+    const f16* src = reinterpret_cast<const f16*>(p.A) + (size_t)(m < p.M ? m : p.M - 1) * p.lda + 8 * hh;
+#pragma unroll
+    for (int s = 0; s < P3KS; ++s) af[s] = *reinterpret_cast<const f16x8*>(src + 16 * s);
+  };
+  // folded LayerNorm statistics: computed in panel_gemm_kernel's lane layout
+  // (4 lanes per row, ln_merge_stats -- bit-identical statistics), then lane
+  // l takes those of its row wave * 32 + (l & 31) = 16 ib + (l & 15) from
+  // lane l & 15, slot ib
+  auto stats_load = [&](int pnl, float2 (&t)[2][8]) __attribute__((always_inline)) {
+    const int l15 = lane & 15, hq = lane >> 4;
+    const float2* st2 = reinterpret_cast<const float2*>(p.lnst_in) + (unsigned)(hq * p.lnst_rows);
+    const int kp = p.lnst_ns >> 2;
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+      const int m = pnl * PBM + wave * 32 + ib * 16 + l15;
+      const int mr = m < p.M ? m : p.M - 1;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) t[ib][k] = st2[(unsigned)((k < kp ? 4 * k : 0) * p.lnst_rows + mr)];
+    }
+  };
+  auto stats_merge = [&](const float2 (&t)[2][8], float& mean_o, float& rstd_o) __attribute__((always_inline)) {
+    const int kp = p.lnst_ns >> 2;
+    const float invd = 1.f / (float)(p.lnst_ns * 32);
+    float mn[2], rs[2];
+#pragma unroll
+    for (int ib = 0; ib < 2; ++ib) {
+      float var;
+      ln_merge_stats(t[ib], kp, invd, mn[ib], var);
+      rs[ib] = rsqrtf(__fadd_rn(var, p.ln_eps));
+    }
+    const int src = lane & 15;
+    const float m0 = __shfl(mn[0], src), m1 = __shfl(mn[1], src);
+    const float r0 = __shfl(rs[0], src), r1 = __shfl(rs[1], src);
+    mean_o = (l31 >> 4) ? m1 : m0;
+    rstd_o = (l31 >> 4) ? r1 : r0;
+  };
+
+  // ---- epilogue of group pair q (0..3) of a unit: n-block nb = q >> 1,
+  // groups g0 = 2 (q & 1) and g0 + 1; the lane holds columns nb * 32 + 8 g +
+  // 4 hh .. +3 of its row for g = g0, g0 + 1.  After the fp32 epilogue one
+  // v_permlane32_swap per 32-bit word gives lane l < 32 the 8 columns of g0
+  // and lane l + 32 those of g0 + 1: a 16-B store per lane, each row's 32
+  // bytes in one instruction (8-B stores were the unit's store-issue bound,
+  // MI355X_MICROARCH.md "attention epilogue store tail" / cdna_hip T21).
+  // Branch-free: rows >= M and a run's first (dummy) epilogue go to the sink.
+  auto epi_pair32 = [&](int q, int pnl, int c, const f32x16 (&accP)[2], float prstd, bool live)
+                        __attribute__((always_inline)) {
+    const int nb = q >> 1, g0 = 2 * (q & 1);
+    f32x2 x[4];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const int g = g0 + e;
+      const float4 b = *reinterpret_cast<const float4*>(tab_b + c * PBN + nb * 32 + 8 * g + 4 * hh);
+      const float v0 = accP[nb][4 * g], v1 = accP[nb][4 * g + 1], v2 = accP[nb][4 * g + 2], v3 = accP[nb][4 * g + 3];
+      if constexpr (FOLD) {
+        x[2 * e] = f32x2{fmaf(prstd, v0, b.x), fmaf(prstd, v1, b.y)};
+        x[2 * e + 1] = f32x2{fmaf(prstd, v2, b.z), fmaf(prstd, v3, b.w)};
+      } else {
+        x[2 * e] = f32x2{v0 + b.x, v1 + b.y};
+        x[2 * e + 1] = f32x2{v2 + b.z, v3 + b.w};
+      }
+    }
+    f32x2 y[4];
+    if constexpr (ACT == ACT_GELU) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) y[i] = gelu_erf2(x[i]);
+    } else if constexpr (ACT == ACT_RELU) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) y[i] = f32x2{x[i][0] > 0.f ? x[i][0] : 0.f, x[i][1] > 0.f ? x[i][1] : 0.f};
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) y[i] = x[i];
+    }
+    const int m = row_of(pnl);
+    const bool ok = live && m < p.M;
+    typedef f16 f16x2 __attribute__((ext_vector_type(2)));
+    auto pk = [](float a, float b) __attribute__((always_inline)) {
+      return __builtin_bit_cast(unsigned, f16x2{(f16)a, (f16)b});
+    };
+    // the 8 columns of group g0 + hh, one 16-B store (A = group g0's words, B = g0 + 1's)
+    auto swap_store = [&](f16* rowbase, float sc) __attribute__((always_inline)) {
+      const unsigned a0 = pk(y[0][0] * sc, y[0][1] * sc), a1 = pk(y[1][0] * sc, y[1][1] * sc);
+      const unsigned b0 = pk(y[2][0] * sc, y[2][1] * sc), b1 = pk(y[3][0] * sc, y[3][1] * sc);
+      const auto s0 = __builtin_amdgcn_permlane32_swap(a0, b0, false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(a1, b1, false, false);
+      const uint4 v = {s0[0], s1[0], s0[1], s1[1]};
+      uint4* dst = ok ? reinterpret_cast<uint4*>(rowbase + nb * 32 + 8 * (g0 + hh)) : g_psink8 + lane;
+      *dst = v;
+    };
+    if constexpr (EM == E_STORE) {
+      swap_store(reinterpret_cast<f16*>(p.out16) + (size_t)(ok ? m : 0) * p.ldo + c * PBN, 1.f);
+    } else {
+      const int which = c / p.heads, hd = c - which * p.heads;
+      const int mm = ok ? m : 0;
+      const int bi = mm / p.T, t = mm - bi * p.T;
+      if (which < 2) {
+        f16* base = which == 0 ? reinterpret_cast<f16*>(p.q) : reinterpret_cast<f16*>(p.k);
+        swap_store(base + ((size_t)(bi * p.heads + hd) * p.Tpad + t) * 64, which == 0 ? p.qscale : 1.f);
+      } else {
+        f16* sink = reinterpret_cast<f16*>(g_psink8 + lane);
+        const size_t tp = p.Tpad;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int n0 = nb * 32 + 8 * (g0 + e) + 4 * hh;
+          f16* row = reinterpret_cast<f16*>(p.vt) + ((size_t)(bi * p.heads + hd) * 64 + n0) * p.Tpad + vt_pos(t);
+          *(ok ? row : sink) = (f16)y[2 * e][0];
+          *(ok ? row + tp : sink) = (f16)y[2 * e][1];
+          *(ok ? row + 2 * tp : sink) = (f16)y[2 * e + 1][0];
+          *(ok ? row + 3 * tp : sink) = (f16)y[2 * e + 1][1];
+        }
+      }
+    }
+  };
+
+  // W fragment addresses: k-step s reads logical chunk 2 (s & 3) + hh of
+  // segment s >> 2 in row nb * 32 + l31, physical chunk (2 (s & 3)) ^ x with
+  // x = hh ^ ((l31 >> 1) & 7): four lane bases, the rest immediates
+  const int xsw = hh ^ ((l31 >> 1) & 7);
+  auto unit = [&](auto off_tag, int slot, f32x16(&accC)[2], const f32x16(&accP)[2], bool epi, int pnl, int pc,
+                  float cmean, float prstd, int cc) __attribute__((always_inline)) {
+    constexpr int OFF = decltype(off_tag)::value;
+    const char* sw = smem + slot * PCHB + l31 * 128;
+    // accumulator start: -mean * c1 of this unit's columns (fold), else 0
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      if constexpr (FOLD) {
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const float4 c1 = *reinterpret_cast<const float4*>(tab_c + cc * PBN + nb * 32 + 8 * g + 4 * hh);
+          accC[nb][4 * g] = -cmean * c1.x;
+          accC[nb][4 * g + 1] = -cmean * c1.y;
+          accC[nb][4 * g + 2] = -cmean * c1.z;
+          accC[nb][4 * g + 3] = -cmean * c1.w;
+        }
+      } else {
+#pragma unroll
+        for (int r = 0; r < 16; ++r) accC[nb][r] = 0.f;
+      }
+    }
+    f16x8 wf[2][2];
+    auto rd = [&](int s, f16x8(&w)[2]) __attribute__((always_inline)) {
+      const char* b = sw + (((2 * (s & 3)) ^ xsw) << 4) + (s >> 2) * 8192;
+      w[0] = *reinterpret_cast<const f16x8*>(b);
+      w[1] = *reinterpret_cast<const f16x8*>(b + 4096);
+    };
+    rd(0, wf[0]);
+#pragma unroll
+    for (int s = 0; s < P3KS; ++s) {
+      if (s + 1 < P3KS) rd(s + 1, wf[(s + 1) & 1]);
+      // the previous unit's epilogue: group pairs q = 0..3 at k-steps OFF + 3 q
+      const int rel = s - OFF;
+      const bool ep = rel >= 0 && rel < 12 && (rel % 3) == 0;
+      accC[0] = pmfma32(wf[s & 1][0], af[s], accC[0]);
+      accC[1] = pmfma32(wf[s & 1][1], af[s], accC[1]);
+      if (ep) epi_pair32(rel / 3, pnl, pc, accP, prstd, epi);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  PTRACE(95, 0)  // (trace builds: kernel entry)
+#if PX_PRIO
+  if (wave >= 4) __builtin_amdgcn_s_setprio(1);
+#endif
+#pragma unroll
+  for (int r = 0; r < PLEAD; ++r)
+    if (r < nu) issue(r);
+  auto run = [&](auto off_tag) __attribute__((always_inline)) {
+    f32x16 acc0[2], acc1[2];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc1[0][r] = acc1[1][r] = 0.f;
+    float lmean = 0.f, lrstd = 1.f;
+    int pc = 0;
+    auto epi_all = [&](const f32x16(&accP)[2], int pnl) __attribute__((always_inline)) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) epi_pair32(q, pnl, pc, accP, lrstd, true);
+    };
+    int j = 0, ppnl = 0;
+    while (j < nu) {
+      const int pnl = (u0 + j) / nch;
+      const int jend = min(nu, (pnl + 1) * nch - u0);
+      if (j > 0) epi_all(acc1, ppnl);
+      PTRACE(j > 0 ? 93 : 91, 0)  // (trace: panel switch / first panel start)
+      // the LN statistics' loads, then the panel's A; wait for everything
+      // older than the 24 A loads (the chunk DMAs in flight, the statistics)
+      // and let the first unit's k-steps wait for their own A fragments (the
+      // compiler counts those loads): the panel load overlaps the unit's
+      // first MFMAs instead of draining in front of them
+      float2 st[2][8];
+      if constexpr (FOLD) stats_load(pnl, st);
+      load_panel(pnl);
+      pwait_vm<P3KS>();
+      if constexpr (FOLD) stats_merge(st, lmean, lrstd);
+      PTRACE(j > 0 ? 94 : 92, 0)  // (trace: statistics landed)
+      const int j0 = j;
+      auto step = [&](int jj, f32x16(&accC)[2], const f32x16(&accP)[2]) __attribute__((always_inline)) {
+        pbarrier();
+        PTRACE(jj, 0)
+        if (jj + PLEAD < nu) issue(jj + PLEAD);
+        const int cc = (u0 + jj) - pnl * nch;
+        unit(off_tag, jj % PSLOTS, accC, accP, jj > j0, pnl, pc, lmean, lrstd, cc);
+        pc = cc;
+        // chunk jj + 1 landed: it was issued at the top of unit jj - 1; since
+        // then units jj - 1 and jj each issued >= 4 stores (one 16-B store per
+        // group pair; E_QKV's V^T chunks 32 scalar ones) and, unless near the
+        // end, chunk jj + 2's 6 DMAs
+        static_assert(PLEAD == 2, "panel32: the counts below assume a 3-slot ring");
+        PTRACE(jj, 1)
+        if (jj + PLEAD < nu) pwait_vm<4 + 6 + 4>();
+        else pwait_vm<4 + 4>();
+        PTRACE(jj, 2)
+      };
+      // the run's first unit peeled off the loop: its k-steps wait for their
+      // own A fragments (a loop would wait for all of them at its head)
+      step(j, acc0, acc1);  // -> acc0
+      ++j;
+      for (; j + 1 < jend; j += 2) {
+        step(j, acc1, acc0);
+        step(j + 1, acc0, acc1);
+      }
+      if (j < jend) {
+        step(j, acc1, acc0);  // -> acc1
+        ++j;
+      } else {
+        acc1[0] = acc0[0];
+        acc1[1] = acc0[1];
+      }
+      ppnl = pnl;
+    }
+    epi_all(acc1, ppnl);
+    pwait_vm0();
+    PTRACE(90, 0)  // (trace: kernel end, stores drained)
+  };
+  if (wave < 4) run(std::integral_constant<int, 0>{});
+  else run(std::integral_constant<int, P3_OFF1>{});
+}
+
+
 }  // namespace
 
 // CUs of the current device, cached per device id (persistent grids size
@@ -630,6 +948,21 @@ hipError_t launch_panel_gemm(const GemmParams& p, hipStream_t st) {
   const int U = nch * npan;
   const int G = U < cu_count() ? U : cu_count();
   const dim3 g(G), b(512);
+  if (knob(KNOB_PANEL32) && (p.emode == E_STORE || p.emode == E_QKV)) {
+    if (p.emode == E_QKV) {
+      if (p.lnst_in) hipLaunchKernelGGL((panel32_kernel<E_QKV, ACT_NONE, true>), g, b, 0, st, p, nch, npan);
+      else hipLaunchKernelGGL((panel32_kernel<E_QKV, ACT_NONE, false>), g, b, 0, st, p, nch, npan);
+    } else if (p.lnst_in) {
+      if (p.act == ACT_GELU) hipLaunchKernelGGL((panel32_kernel<E_STORE, ACT_GELU, true>), g, b, 0, st, p, nch, npan);
+      else if (p.act == ACT_RELU) hipLaunchKernelGGL((panel32_kernel<E_STORE, ACT_RELU, true>), g, b, 0, st, p, nch, npan);
+      else hipLaunchKernelGGL((panel32_kernel<E_STORE, ACT_NONE, true>), g, b, 0, st, p, nch, npan);
+    } else {
+      if (p.act == ACT_GELU) hipLaunchKernelGGL((panel32_kernel<E_STORE, ACT_GELU, false>), g, b, 0, st, p, nch, npan);
+      else if (p.act == ACT_RELU) hipLaunchKernelGGL((panel32_kernel<E_STORE, ACT_RELU, false>), g, b, 0, st, p, nch, npan);
+      else hipLaunchKernelGGL((panel32_kernel<E_STORE, ACT_NONE, false>), g, b, 0, st, p, nch, npan);
+    }
+    return hipGetLastError();
+  }
   if (p.emode == E_RESID) {
     hipLaunchKernelGGL((panel_gemm_kernel<E_RESID, ACT_NONE, false>), g, b, 0, st, p, nch, npan);
   } else if (p.emode == E_QKV) {

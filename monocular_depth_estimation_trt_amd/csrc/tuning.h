@@ -42,6 +42,15 @@ enum Knob : int {
   // E_QKV problems at large batch -- the ViT-S fc1 and qkv (1: on; 2: also
   // the f16-residual proj, slower in the engine).  test_panel_gemm_bit_exact
   KNOB_PANEL,
+  // the panel GEMM's qkv / fc1 on v_mfma_f32_32x32x16_f16 with the folded
+  // LayerNorm's mean term in the accumulator's initial value (panel32_kernel;
+  // 1: on; default off: no step gain, gemm_panel.hip).
+  // test_panel32_matches_tile_kernel
+  KNOB_PANEL32,
+  // small-grid residual updates (ViT-S batch 1: fc2 / proj, 1370 x 384) on
+  // 32 x 64 tiles with the whole K loop and a 4-deep ring instead of split-K
+  // slices + the reduce launch (1: on).  test_narrow_resid_matches_split
+  KNOB_NARROW_RESID,
   KNOB_COUNT
 };
 

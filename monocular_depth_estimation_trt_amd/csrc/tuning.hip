@@ -29,6 +29,8 @@ constexpr KnobDef kKnobs[KNOB_COUNT] = {
     {"w8small", "MDE_W8SMALL", 1, 0, 1},
     {"conv_persist", "MDE_CONV_PERSIST", 1, 0, 2},
     {"panel", "MDE_PANEL", 1, 0, 2},
+    {"panel32", "MDE_PANEL32", 0, 0, 1},
+    {"narrow_resid", "MDE_NARROW_RESID", 1, 0, 1},
 };
 
 std::atomic<int> g_val[KNOB_COUNT];

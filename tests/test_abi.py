@@ -78,7 +78,7 @@ def test_tuning_switches(lib_path):
     from monocular_depth_estimation_trt_amd import _lib
     L = _lib.lib()
     for name in _lib.TUNING:
-        assert _lib.get_tuning(name) == 1, name
+        assert _lib.get_tuning(name) == _lib.TUNING_DEFAULT.get(name, 1), name
     v = ctypes.c_int()
     assert L.mde_tuning_get(b"no_such_switch", ctypes.byref(v)) == 5
     assert L.mde_tuning_set(b"splitk", 2) == 1

@@ -165,10 +165,21 @@ def test_engine_reference_size_sweep_vs_oracle(gpu, h, w, B):
     cfg = weights.model_config("vits", "metric")
     sd = weights.synthetic_state_dict(cfg, 392 + w)
     x = weights.synthetic_images(B, h, w, first_seed=7)
-    ref = dav2_ref.forward(dav2_ref.to_torch(sd), cfg, x).numpy()
+    W = dav2_ref.to_torch(sd)
+    ref = dav2_ref.forward(W, cfg, x).numpy()
     y = run_engine(pack.pack_bytes(sd, cfg, h, w), x)
     assert y.shape == (B, h, w)
-    check(y, ref, 20.0, f"{h}x{w} B={B} vs oracle")
+    # per-pixel bar derived from the attribution (VERDICT r05 item 3,
+    # test_engine_worst_pixel_attribution): an IDEAL fp16 engine -- fp16
+    # weights and fp16 storage where this engine stores fp16, fp32 arithmetic
+    # otherwise -- is already 0.046 m from the fp32 oracle here (sigmoid *
+    # 20 m at logits near 0); the engine may be up to 1.5x that, and never
+    # held to less than the 0.3 %-of-max-depth bar
+    import numerics_f16 as N
+    e16 = float(np.abs(N.forward(W, cfg, x, N.STAGES)[0].numpy() - ref).max())
+    extra = max(0.0, 1.5 * e16 - TOL["vits"][1] * 20.0)
+    print(f"{h}x{w}: ideal-fp16 max |d| {e16:.4f} m -> max-abs bar {TOL['vits'][1] * 20.0 + extra:.4f} m")
+    check(y, ref, 20.0, f"{h}x{w} B={B} vs oracle", extra_abs=extra)
 
 
 @pytest.mark.parametrize("h,w,B", [(392, 518, 2), (672, 896, 1), (518, 518, 2)])
@@ -217,6 +228,31 @@ def test_engine_worst_pixel_attribution(gpu, h, w, B):
     # fp16 storage explains the error scale: the engine is within 1.5x of it
     assert d_eng.max() <= 1.5 * d_sto.max() + 0.005, (d_eng.max(), d_sto.max())
     assert d_e16.max() <= 1.5 * d_sto.max() + 0.005, (d_e16.max(), d_sto.max())
+
+
+def test_narrow_resid_matches_split(gpu):
+    """Switch "narrow_resid" (gemm.hip): ViT-S 518^2 batch 1 runs fc2 and proj
+    on 32 x 64 tiles with the whole K loop instead of split-K slices + the
+    reduce launch.  Another fp32 association of the same sums: the two depth
+    maps agree to fp16-storage noise (measured rel_mean 5.5e-4, max 0.040 m),
+    and the narrow path meets the oracle bars."""
+    from oracle import dav2_ref
+    cfg = weights.model_config("vits", "metric")
+    sd = weights.synthetic_state_dict(cfg, 77)
+    x = weights.synthetic_images(1, 518, 518, first_seed=5)
+    blob = pack.pack_bytes(sd, cfg, 518, 518)
+    with _lib.tuning(narrow_resid=0):
+        y0 = run_engine(blob, x)
+    with _lib.tuning(narrow_resid=1):
+        y1 = run_engine(blob, x)
+    m = depth_metrics(y1, y0)
+    print("narrow vs split", m)
+    # two fp32 associations, each ~4e-4 (rel_mean) from the fp32 oracle by
+    # fp16 storage (test_numerics_attribution): their difference is that
+    # noise twice over, not a bias
+    assert m["rel_mean"] < 1.2e-3 and m["max_abs"] < 0.08 and m["corr"] > 0.99999, m
+    ref = dav2_ref.forward(dav2_ref.to_torch(sd), cfg, x).numpy()
+    check(y1, ref, 20.0, "narrow_resid B=1 vs oracle")
 
 
 def test_batch_and_graph_consistency(gpu):

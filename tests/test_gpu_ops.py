@@ -196,6 +196,74 @@ def test_panel_gemm_bit_exact(gpu, case):
             f"{case}: panel kernel {name} differs from the 128^2 kernel ({int((d > 0).sum())} elements, max {float(d.max())})"
 
 
+@pytest.mark.parametrize("case", ["linear_gelu", "linear_none", "linear_relu_tail", "lnfold_gelu",
+                                  "qkv_1370", "qkv_37", "qkv_lnfold"])
+def test_panel32_matches_tile_kernel(gpu, case):
+    """Switch "panel32" (gemm_panel.hip panel32_kernel: v_mfma_f32_32x32x16,
+    the folded LayerNorm's mean term in the accumulator's initial value, 16-B
+    stores through v_permlane32_swap) against the 128^2 kernel: another fp32 association of the same sums, so
+    every output within the f16 output rounding (2 ulp relative + 1e-3),
+    no nearer the float64 reference's error than 1.25x the 128^2 kernel's
+    (LN fold cases), and bit-identical from run to run."""
+    from monocular_depth_estimation_trt_amd import _lib
+    k = 384
+
+    def run(cfg):
+        with _lib.tuning(**cfg):
+            if case.startswith("qkv"):
+                q = torch.zeros(B * H, Tp, 64, dtype=torch.float16, device=gpu)
+                kk = torch.zeros_like(q)
+                vt = torch.zeros(B * H, 64, Tp, dtype=torch.float16, device=gpu)
+                if case == "qkv_lnfold":
+                    op("mde_op_qkv_lnfold", ptr(x), ptr(part), 1e-6, ptr(wp), wp.shape[1], ptr(c1), ptr(b), B, T, H,
+                       Tp, 0.125, ptr(q), ptr(kk), ptr(vt), stream())
+                else:
+                    op("mde_op_qkv", ptr(x), ptr(wp), wp.shape[1], ptr(b), B, T, H, Tp, 0.125, ptr(q), ptr(kk),
+                       ptr(vt), stream())
+                return torch.cat([q.flatten(), kk.flatten(), vt.flatten()])
+            out = torch.full((m, n), float("nan"), dtype=torch.float16, device=gpu)
+            if case == "lnfold_gelu":
+                op("mde_op_linear_lnfold", ptr(x), ptr(part), 1e-6, ptr(wp), wp.shape[1], ptr(c1), ptr(b), m, n, k,
+                   act, ptr(out), n, stream())
+            else:
+                op("mde_op_linear", ptr(x), k, ptr(wp), wp.shape[1], m, n, k, ptr(b), act, ptr(out), n, stream())
+            return out.flatten()
+
+    if case.startswith("qkv"):
+        B, T, H = {"qkv_1370": (16, 1370, 6), "qkv_37": (480, 37, 6), "qkv_lnfold": (16, 1370, 6)}[case]
+        Tp = -(-T // 64) * 64
+        m, n = B * T, 3 * 64 * H
+    else:
+        m = {"linear_gelu": 16384, "linear_none": 21920, "linear_relu_tail": 16397, "lnfold_gelu": 38360}[case]
+        n = 1536 if case != "linear_none" else 1152
+        act = {"linear_gelu": 2, "linear_none": 0, "linear_relu_tail": 1, "lnfold_gelu": 2}[case]
+    x = (rn(m, k) * 2 + 0.3).half().to(gpu)
+    w, b = rn(n, k, scale=k ** -0.5), rn(n, scale=0.1).to(gpu)
+    wp = pad_w(w).to(gpu)
+    part = ln_partials_ref(x.cpu()).float().to(gpu)
+    c1 = rn(n).to(gpu)
+    y32 = run({"panel": 1, "panel32": 1})
+    y32b = run({"panel": 1, "panel32": 1})
+    y0 = run({"panel": 0, "panel32": 0})
+    assert torch.isfinite(y32).all(), case
+    assert torch.equal(y32, y32b), f"{case}: panel32 not deterministic"
+    d = (y32.float() - y0.float()).abs()
+    lim = 1e-3 + 2.0 ** -9 * y0.float().abs()
+    bad = int((d > lim).sum())
+    print(f"{case}: {int((d > 0).sum())} of {d.numel()} outputs differ from the 128^2 kernel, max {float(d.max()):.3g}")
+    assert bad == 0, f"{case}: {bad} outputs beyond 2 f16 ulp (max {float(d.max())})"
+    if case in ("lnfold_gelu", "qkv_lnfold") and not case.startswith("qkv"):
+        xr = x.double().cpu()[:4096]
+        mu = xr.mean(1, keepdim=True)
+        rs = 1.0 / torch.sqrt(((xr - mu) ** 2).mean(1, keepdim=True) + 1e-6)
+        acc = xr @ wp[:, :k].double().cpu()[:n].T
+        ref = F.gelu(rs * (acc - mu * c1.double().cpu()[None, :]) + b.double().cpu()[None, :])
+        e32 = (y32.reshape(m, n)[:4096].double().cpu() - ref).abs().sum().item()
+        e0 = (y0.reshape(m, n)[:4096].double().cpu() - ref).abs().sum().item()
+        print(f"{case}: |panel32 - f64| {e32:.6g}  |128^2 - f64| {e0:.6g}")
+        assert e32 <= 1.25 * e0, (e32, e0)
+
+
 LOG2E = 1.4426950408889634
 
 

@@ -44,7 +44,7 @@ def main():
     fn.argtypes = [C.c_void_p]
     assert fn(buf.ctypes.data) == 0
     t = buf.astype(np.int64)
-    nseg = int((t[0, 0, :, 0] > 0).sum())
+    nseg = int((t[0, 0, :90, 0] > 0).sum())
     print(f"units recorded per wave: {nseg}")
     rows = []
     for blk in range(8):
@@ -70,6 +70,20 @@ def main():
     if ck:
         print(f"in-kernel clock {np.median(ck):.3f} GHz (median over waves); units {nseg}, "
               f"first -> last unit start {np.median([(t[b, 0, nseg - 1, 3] - t[b, 0, 0, 3]) / 100.0 for b in range(8)]):.1f} us")
+    # whole-kernel phases (panel32 trace builds): realtime stamps, us
+    rt = t[:, :, :, 3].astype(np.float64) / 100.0
+    if (t[:, :, 95, 3] > 0).all():
+        ent, p0, p1, end = rt[:, :, 95], rt[:, :, 91], rt[:, :, 92], rt[:, :, 90]
+        u0 = rt[:, :, 0]
+        print(f"per wave (median over blocks 0-7, us): entry -> first panel load start {np.median(p0 - ent):.2f}, "
+              f"first panel load {np.median(p1 - p0):.2f}, -> first unit {np.median(u0 - p1):.2f}; "
+              f"entry -> end {np.median(end - ent):.2f}")
+        sw = t[:, :, 93, 3] > 0
+        if sw.any():
+            print(f"mid-run panel switch (epilogue + A load + stats + drain): "
+                  f"{np.median((rt[:, :, 94] - rt[:, :, 93])[sw]):.2f} us over {int(sw.sum())} waves")
+        print(f"spread of kernel-entry times over blocks 0-7: {ent[:, 0].max() - ent[:, 0].min():.2f} us; "
+              f"of end times {end[:, 0].max() - end[:, 0].min():.2f} us")
     lo = np.array([(t[b, :4, 1:nseg - 1, 1] - t[b, :4, 1:nseg - 1, 0]).mean() for b in range(8)])
     hi = np.array([(t[b, 4:, 1:nseg - 1, 1] - t[b, 4:, 1:nseg - 1, 0]).mean() for b in range(8)])
     print(f"work per unit: waves 0-3 {lo.mean():7.0f}  waves 4-7 {hi.mean():7.0f}")
