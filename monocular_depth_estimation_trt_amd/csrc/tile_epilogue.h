@@ -206,6 +206,10 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
   static_assert(TN >= 1 && C % 8 == 0, "tile");
   if constexpr (EM != E_STORE && EM != E_RESID && EM != E_QKV && EM != E_CONVT && EM != E_PATCH) {
     return false;
+  } else if constexpr ((CPR & (CPR - 1)) != 0 || (CHR & (CHR - 1)) != 0) {
+    // the row swizzles and the read-back geometry need power-of-two chunk
+    // counts per row (a 48-column wave tile, TN = 3, takes the direct path)
+    return false;
   } else {
     if constexpr (EM == E_RESID || EM == E_PATCH) {
       if (p.lnst_out && (C % 32)) return false;  // LN partials need whole 32-column slices per wave
