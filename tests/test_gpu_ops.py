@@ -667,10 +667,13 @@ def test_upconv_matches_conv3(gpu, B, sh, sw, uh, uw, cin, head):
     """The separable upsampling conv (conv.hip upconv_kernel: one tile per
     workgroup on small grids, persistent when the grid exceeds what the chip
     holds at once -- the last two cases) against the 4-tap conv3_kernel it
-    replaces (switch "upconv" = 0): the same two-level f16 blend in the same
-    order, so at 32 input channels (one chunk, same MFMA order) the outputs
-    are bit-identical; wider inputs sum 32-channel chunks in another order
-    (fp32), within one f16 ulp."""
+    replaces (switch "upconv" = 0) and an fp32 torch reference: the same
+    two-level f16 blend in the same order, so at 32 input channels (one
+    chunk, same MFMA order) the outputs are bit-identical; wider inputs sum
+    32-channel chunks in another order (fp32).  Both paths are held to the
+    fp32 reference (upconv's mean |error| within 1.1x of conv3's, max within
+    2x) -- round 6 measured a matrix-core vertical blend against this bar
+    (slower, not kept: DESIGN.md section 9)."""
     from monocular_depth_estimation_trt_amd import _lib
     x = rn(B, cin, sh, sw)
     w1, b1 = rn(32, cin, 3, 3, scale=(9 * cin) ** -0.5), rn(32, scale=0.02)
@@ -691,6 +694,18 @@ def test_upconv_matches_conv3(gpu, B, sh, sw, uh, uw, cin, head):
             torch.cuda.synchronize()
         outs.append(out.float().cpu())
     old, new = outs
+    xr = xin.float().cpu().permute(0, 3, 1, 2)
+    up = F.interpolate(xr, size=(uh, uw), mode="bilinear", align_corners=True)
+    hid = F.conv2d(up, w1.half().float(), b1, padding=1)
+    if head:
+        ref = torch.sigmoid(F.conv2d(F.relu(hid), w2.reshape(1, 32, 1, 1)) + 0.05)[:, 0] * 20.0
+    else:
+        ref = hid.permute(0, 2, 3, 1)
+    e_old, e_new = (old - ref).abs(), (new - ref).abs()
+    print(f"upconv vs fp32: mean {float(e_new.mean()):.3g} max {float(e_new.max()):.3g}; conv3: mean "
+          f"{float(e_old.mean()):.3g} max {float(e_old.max()):.3g}")
+    assert float(e_new.mean()) <= 1.1 * float(e_old.mean()) + 1e-6, (e_new.mean(), e_old.mean())
+    assert float(e_new.max()) <= 2.0 * float(e_old.max()) + 1e-4, (e_new.max(), e_old.max())
     if cin == 32:
         assert torch.equal(old, new), (old - new).abs().max()
     else:
