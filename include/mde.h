@@ -103,7 +103,11 @@ const char* mde_last_error(void);
  * small-grid 64^2 tiles; "w8small" (0-1, 1) 8-wave small-grid 128^2 tiles;
  * "conv_persist" (0-2, 1) persistent 64-channel RCU conv (1: 16 x 16 tiles,
  * 2: 8 x 16); "panel" (0-2, 1) A-stationary panel GEMM for the K = 384
- * qkv / fc1 at large batch (2: also the f16-residual proj).  The environment variable of a switch is exactly
+ * qkv / fc1 at large batch (2: also the f16-residual proj); "panel32" (0-1,
+ * 0) that GEMM on 32x32x16 MFMAs with the LN fold's mean term in the
+ * accumulator's initial value (within 1 f16 ulp of the default); "narrow_resid"
+ * (0-1, 1) 32 x 64 whole-K tiles for small-grid residual updates instead of
+ * split-K + reduce.  The environment variable of a switch is exactly
  * MDE_ + its name upper-cased (MDE_DEEP64, MDE_W8SMALL, ...); a value that is
  * not an integer in range is reported on stderr and ignored.
  * Every setting computes the same depth map within the stated tolerance; the

@@ -65,9 +65,8 @@ constexpr int PNMAX = 1536;          // widest N (bias / lnc1 table)
 constexpr int PTAB = PSLOTS * PCHB;  // bias / lnc1 table offset
 constexpr int PLDS = PTAB + 2 * PNMAX * 4;  // 156 KB at 3 slots (108 KB at 2)
 static_assert(PLDS <= 163840, "LDS");
-#ifndef PX_PACKED
-#define PX_PACKED 1  // 1: the epilogue's fp32 arithmetic on packed f32 pairs (v_pk_*_f32)
-#endif
+// (round 6: the GELU on scalar registers instead of packed f32 pairs spilled
+// 41 VGPRs in the LN-fold fc1 and ran slower; the packed form stays)
 #ifndef PEPI_STRIDE
 #define PEPI_STRIDE 1  // k-substeps between the epilogue's block pairs
 #endif
@@ -366,34 +365,7 @@ __global__ void __launch_bounds__(512) panel_gemm_kernel(const GemmParams p, int
       x[2 * e + 1] = f32x2{v[2], v[3]};
     }
     f32x2 y[4];
-    if constexpr (ACT == ACT_GELU && !PX_PACKED) {
-      // gelu_erf per value, the 8 values' chains in lockstep: the fused
-      // operations of gelu_erf2 in the same order on scalar registers (packed
-      // f32 VALU beside MFMAs costs more issue time than the two scalar ops,
-      // MI355X_MICROARCH.md cycle constants)
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {  // one block's 4 values per pass (8 chains spill the fold kernels)
-        float xv[4], xc[4], x2[4], t[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) xv[i] = x[2 * e + (i >> 1)][i & 1];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) xc[i] = __builtin_amdgcn_fmed3f(xv[i], -8.f, 8.f);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) x2[i] = __fmul_rn(xc[i], xc[i]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) t[i] = fmaf(0.001014263055f, x2[i], -0.106775724f);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) t[i] = fmaf(t[i], x2[i], -2.301121339f);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) t[i] = __fmul_rn(xc[i], t[i]);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) t[i] = __fadd_rn(1.f, __builtin_amdgcn_exp2f(t[i]));
-#pragma unroll
-        for (int i = 0; i < 4; ++i) t[i] = __builtin_amdgcn_rcpf(t[i]);
-        y[2 * e] = f32x2{__fmul_rn(xv[0], t[0]), __fmul_rn(xv[1], t[1])};
-        y[2 * e + 1] = f32x2{__fmul_rn(xv[2], t[2]), __fmul_rn(xv[3], t[3])};
-      }
-    } else if constexpr (ACT == ACT_GELU) {
+    if constexpr (ACT == ACT_GELU) {
       const f32x2 cc = {0.001014263055f, 0.001014263055f}, cb2 = {-0.106775724f, -0.106775724f},
                   ca = {-2.301121339f, -2.301121339f};
       f32x2 xc[4], x2[4], t[4], d[4];
