@@ -107,7 +107,8 @@ const char* mde_last_error(void);
  * 0) that GEMM on 32x32x16 MFMAs with the LN fold's mean term in the
  * accumulator's initial value (within 1 f16 ulp of the default); "narrow_resid"
  * (0-1, 1) 32 x 64 whole-K tiles for small-grid residual updates instead of
- * split-K + reduce.  The environment variable of a switch is exactly
+ * split-K + reduce; "attn16" (0-1, 1) the large-grid attention on 16x16x32
+ * MFMAs (same softmax, other summation grouping).  The environment variable of a switch is exactly
  * MDE_ + its name upper-cased (MDE_DEEP64, MDE_W8SMALL, ...); a value that is
  * not an integer in range is reported on stderr and ignored.
  * Every setting computes the same depth map within the stated tolerance; the
@@ -211,8 +212,8 @@ int mde_op_attention_ws(const void* q_f16, const void* k_f16, const void* vt_f16
                         int tokens, int tokens_pad, int ldo, void* ws, size_t ws_bytes, void* stream);
 size_t mde_op_attention_ws_bytes(int batch, int heads, int tokens);
 /* mde_op_attention_ws with an explicit launch configuration (tests / tuning; no reference
- * counterpart): cfg = "<waves>[s<split>][g<groups>][r<ring>][q2]", e.g. "8" (256-query
- * workgroups), "4s2" (split-KV over two workgroups + merge kernel, needs ws), "4g2" (two key
+ * counterpart): cfg = "<waves>[s<split>][g<groups>][r<ring>][q2][m]", e.g. "8" (256-query
+ * workgroups), "8m" (the same on 16x16x32 MFMAs, unsplit 4 / 8 waves only), "4s2" (split-KV over two workgroups + merge kernel, needs ws), "4g2" (two key
  * groups of 64 queries inside one workgroup, merged through LDS); NULL or "" = the launcher's
  * policy. */
 int mde_op_attention_cfg(const void* q_f16, const void* k_f16, const void* vt_f16, void* o_f16, int batch, int heads,

@@ -40,6 +40,11 @@
 // writing its unnormalised fp32 O with its running max and sum for
 // attn_combine_kernel to merge.
 //
+// Large grids (B = 48: 8 waves, unsplit) run attn16_fwd_kernel by default
+// (switch "attn16", round 6): the same loop on v_mfma_f32_16x16x32_f16, see
+// its comment -- 158 vs 167 us standalone at B = 48, step +0.5-0.9 % in four
+// same-box pairs.
+//
 // Measured alternatives (MI355X, B = 28): two 32-query
 // sub-blocks per wave (256 VGPRs), 128-key tiles, one-block software
 // pipelining, an 8-wave ping-pong of MFMA / softmax segments and a lagged
@@ -55,6 +60,7 @@
 
 #include "mde_device.h"
 #include "mde_ops.h"
+#include "tuning.h"
 
 namespace mde {
 
@@ -477,6 +483,239 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
   }
 }
 
+// ---- The same loop on v_mfma_f32_16x16x32_f16 (switch "attn16", cfg "<NW>m") ----
+//
+// Per 32-key block and 32-query wave the work is that of attn_fwd_kernel --
+// 256 cycles of matrix pipe, 16 v_exp per lane, the same LDS reads -- but
+// the products are 8 + 8 MFMAs of 16 cycles with at most two dependent ones
+// per accumulator (the 32x32x16 form chains four 32-cycle MFMAs per score
+// tile): the score -> softmax -> P.V chain of a block is shorter, and the
+// smaller shape is the one MI355X_MICROARCH.md (DVFS item 7) measured
+// holding a higher clock under load.  Layout per wave: two query sub-tiles of
+// 16 (s), two key sub-tiles of 16 per block (t); lane l holds query
+// 16 s + (l & 15) and, of key sub-tile t, keys 8 t + 16 (g >> 1) + 4 (g & 1)
+// + r (g = l >> 4, r = 0..3) -- the K rows are fed to the score MFMA's A
+// operand in that order, so the accumulators of t = 0, 1 are directly the
+// P^T B operand of the P.V MFMA against the unchanged V^T layout (vt_pos).
+// The running max rides in the score C operand (one 4-register copy per
+// query sub-tile serves both key sub-tiles); a query's keys sit in four lane
+// groups, so the rare rescale's row max and the final row sum reduce with
+// v_permlane32_swap + v_permlane16_swap.
+MDE_DEV int swz16(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+MDE_DEV float grp4(float x, bool sum) {  // max / sum over lanes (l & 15) + 16 g, g = 0..3
+  auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  x = sum ? __uint_as_float(a[0]) + __uint_as_float(a[1]) : fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  auto c = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
+  return sum ? __uint_as_float(c[0]) + __uint_as_float(c[1]) : fmaxf(__uint_as_float(c[0]), __uint_as_float(c[1]));
+}
+
+template <int NW>
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4, 8)))
+attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16* __restrict__ vt,
+                  f16* __restrict__ o, int H, int T, int Tpad, int ldo) {
+  static_assert(NW == 4 || NW == 8, "waves per workgroup");
+  constexpr int BQ = QW * NW;
+  constexpr int INS = 8 / NW;  // glds row groups per wave per 64-row image
+  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  const int nqb = gridDim.x;
+  const int lin = xcd_remap(blockIdx.y * nqb + blockIdx.x, nqb * gridDim.y);
+  const int bh = lin / nqb;
+  const int b = bh / H, h = bh - (bh / H) * H;
+  const int qbase = (lin - bh * nqb) * BQ + wave * QW;
+  const bool active = qbase < T;
+  const int l15 = lane & 15, g = lane >> 4;
+  const int nkt = (T + KT - 1) / KT;
+
+  const f16* qb = q + (size_t)bh * Tpad * 64;
+  const f16* kb = k + (size_t)bh * Tpad * 64;
+  const f16* vb = vt + (size_t)bh * 64 * Tpad;
+
+  // Q^T (B operand) of sub-tile s, dim step d: lane holds Q[16 s + l15][32 d + 8 g + j]
+  f16x8 qf[2][2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const int qi = qbase + 16 * s + l15;
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+      qf[s][d] = qi < Tpad ? *reinterpret_cast<const f16x8*>(qb + (size_t)qi * 64 + 32 * d + 8 * g) : zero8();
+  }
+
+  const int lrow = lane >> 3, pc = lane & 7;
+  auto issue = [&](int kt, int slot) {
+    char* sK = smem + slot * SLOT;
+    char* sV = sK + TILE_B;
+#pragma unroll
+    for (int i = 0; i < INS; ++i) {
+      const int gg = wave + i * NW;  // 8-row group
+      const int row = gg * 8 + lrow;
+      const int lc = pc ^ lrow;      // swz16: row & 7 == lrow
+      __builtin_amdgcn_global_load_lds(kb + (size_t)(kt * KT + row) * 64 + lc * 8, sK + gg * 8 * 128, 16, 0, 0);
+      __builtin_amdgcn_global_load_lds(vb + (size_t)row * Tpad + kt * KT + lc * 8, sV + gg * 8 * 128, 16, 0, 0);
+    }
+  };
+
+  float m_run[2] = {0.f, 0.f}, l_run[2] = {0.f, 0.f};
+  f32x4 negm[2], acc[4][2];
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    negm[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) acc[dt][s] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  // K row (within the 64-key tile) that A-operand row l15 of key sub-tile t of block kb2 reads
+  const int krow0 = ((l15 >> 3) << 4) + (l15 & 7);
+
+  struct Sc16 {
+    f32x4 v[2][2];  // [t][s]: S'^T = K Q^T - m_run
+  };
+  auto scores = [&](const char* K_, int kt, int kb2, auto first_tag) {
+    constexpr bool FIRST = decltype(first_tag)::value;
+    Sc16 sc;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) sc.v[t][s] = FIRST ? f32x4{0.f, 0.f, 0.f, 0.f} : negm[s];
+#pragma unroll
+    for (int d = 0; d < 2; ++d)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        const f16x8 kf = *reinterpret_cast<const f16x8*>(K_ + swz16(kb2 * 32 + 8 * t + krow0, 4 * d + g));
+#pragma unroll
+        for (int s = 0; s < 2; ++s) sc.v[t][s] = mfma16x16x32(kf, qf[s][d], sc.v[t][s]);
+      }
+    return sc;
+  };
+  // keys >= T -> -inf (last, partial block; a separate step so the branch
+  // does not cut the score MFMAs off the code they are scheduled with)
+  auto mask = [&](Sc16& sc, int kt, int kb2) {
+    if (kt * KT + kb2 * 32 + 32 > T) {
+      const int key0 = kt * KT + kb2 * 32 + 16 * (g >> 1) + 4 * (g & 1);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (key0 + 8 * t + r >= T) {
+            sc.v[t][0][r] = -INFINITY;
+            sc.v[t][1][r] = -INFINITY;
+          }
+    }
+  };
+  // online softmax of one block's scores: the running max (rescale when it
+  // grows past RESCALE_T), then P = exp2(S') as the P.V B operand and the row sums
+  auto rescale = [&](Sc16& sc, auto first_tag) {
+    constexpr bool FIRST = decltype(first_tag)::value;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float mx = fmaxf(fmaxf(sc.v[0][s][0], sc.v[0][s][1]), sc.v[0][s][2]);
+      mx = fmaxf(fmaxf(mx, sc.v[0][s][3]), sc.v[1][s][0]);
+      mx = fmaxf(fmaxf(mx, sc.v[1][s][1]), sc.v[1][s][2]);
+      mx = fmaxf(mx, sc.v[1][s][3]);
+      if (FIRST || __any(mx > RESCALE_T)) {
+        mx = grp4(mx, false);  // the query's block max (relative to m_run)
+        const float delta = FIRST ? mx : fmaxf(mx, 0.f);
+        m_run[s] += delta;
+        negm[s] = f32x4{-m_run[s], -m_run[s], -m_run[s], -m_run[s]};
+        sc.v[0][s] -= delta;
+        sc.v[1][s] -= delta;
+        if (!FIRST) {
+          const float alpha = __builtin_amdgcn_exp2f(-delta);
+          l_run[s] *= alpha;
+#pragma unroll
+          for (int dt = 0; dt < 4; ++dt) acc[dt][s] *= alpha;
+        }
+      }
+    }
+  };
+  struct Pb16 {
+    f16x8 v[2];
+  };
+  auto probs = [&](const Sc16& sc) {
+    Pb16 pb;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float ls0, ls1;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const float p0 = __builtin_amdgcn_exp2f(sc.v[0][s][r]), p1 = __builtin_amdgcn_exp2f(sc.v[1][s][r]);
+        ls0 = r ? ls0 + p0 : p0;
+        ls1 = r ? ls1 + p1 : p1;
+        pb.v[s][r] = (f16)p0;
+        pb.v[s][4 + r] = (f16)p1;
+      }
+      l_run[s] += ls0 + ls1;
+    }
+    return pb;
+  };
+  // O^T[16 dt + 4 g + r][query] += V^T[16 dt + l15][key slot 32 kb2 + 8 g + j] P^T
+  auto pv = [&](const Pb16& pb, const char* V_, int kb2) {
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt) {
+      const f16x8 vf = *reinterpret_cast<const f16x8*>(V_ + swz16(16 * dt + l15, 4 * kb2 + g));
+#pragma unroll
+      for (int s = 0; s < 2; ++s) acc[dt][s] = mfma16x16x32(vf, pb.v[s], acc[dt][s]);
+    }
+  };
+  using NF = std::false_type;
+  auto step = [&](int kt, auto slot_tag, auto first_tag) {
+    constexpr int SL = decltype(slot_tag)::value;
+    if (kt + 1 < nkt) issue(kt + 1, SL ^ 1);  // into the slot of tile kt - 1 (released by the last barrier)
+    if (active) {
+      const char* K_ = smem + SL * SLOT;
+      Sc16 s0 = scores(K_, kt, 0, first_tag);
+      mask(s0, kt, 0);
+      rescale(s0, first_tag);
+      // block 1's score MFMAs (against the updated max) are independent of
+      // block 0's exp2 chain: with the masking branch moved after them, hipcc
+      // interleaves the two (one MFMA per 3-4 VALU)
+      Sc16 s1 = scores(K_, kt, 1, NF{});
+      const Pb16 p0 = probs(s0);
+      pv(p0, K_ + TILE_B, 0);
+      mask(s1, kt, 1);
+      rescale(s1, NF{});
+      pv(probs(s1), K_ + TILE_B, 1);
+    }
+    wait_vm_n<0>();
+    lds_barrier();
+  };
+  using S0 = std::integral_constant<int, 0>;
+  using S1 = std::integral_constant<int, 1>;
+  issue(0, 0);
+  wait_vm_n<0>();
+  lds_barrier();
+  step(0, S0{}, std::true_type{});
+  int kt = 1;
+  for (; kt + 2 <= nkt; kt += 2) {
+    step(kt, S1{}, NF{});
+    step(kt + 1, S0{}, NF{});
+  }
+  if (kt < nkt) step(kt, S1{}, NF{});
+  if (!active) return;
+
+  // epilogue: lane holds O^T[16 dt + 4 g + r][16 s + l15]; lane groups g, g ^ 1
+  // exchange (v_permlane16_swap) so each lane stores 8 consecutive dh (16 B)
+#pragma unroll
+  for (int s = 0; s < 2; ++s) {
+    const float inv = 1.f / grp4(l_run[s], true);
+    const int qs = qbase + 16 * s + l15;
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      const f32x4 a = acc[2 * p][s], c = acc[2 * p + 1][s];
+      const unsigned ax = pack2(a[0] * inv, a[1] * inv), ay = pack2(a[2] * inv, a[3] * inv);
+      const unsigned cx = pack2(c[0] * inv, c[1] * inv), cy = pack2(c[2] * inv, c[3] * inv);
+      auto sx = __builtin_amdgcn_permlane16_swap(ax, cx, false, false);
+      auto sy = __builtin_amdgcn_permlane16_swap(ay, cy, false, false);
+      if (qs < T)
+        *reinterpret_cast<uint4*>(o + ((size_t)b * T + qs) * ldo + h * 64 + 32 * p + 16 * (g & 1) + 8 * (g >> 1)) =
+            make_uint4(sx[0], sy[0], sx[1], sy[1]);
+    }
+  }
+}
+
 // Merge S split-KV partials: one thread per (sequence*head, query, 8 dims).
 // O = sum_s 2^(m_s - m) O_s / sum_s 2^(m_s - m) l_s, m = max_s m_s.
 __global__ void __launch_bounds__(256) attn_combine_kernel(SplitWs ws, int S, int BH, int H, int T, int ldo,
@@ -559,6 +798,16 @@ hipError_t run_attn_grp(const h16* q, const h16* k, const h16* vt, h16* o, int B
   return hipGetLastError();
 }
 
+template <int NW>
+hipError_t run_attn16(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T, int Tpad, int ldo,
+                      hipStream_t st) {
+  const int nqb = (T + QW * NW - 1) / (QW * NW);
+  hipLaunchKernelGGL((attn16_fwd_kernel<NW>), dim3(nqb, B * H), dim3(NW * 64), 0, st, reinterpret_cast<const f16*>(q),
+                     reinterpret_cast<const f16*>(k), reinterpret_cast<const f16*>(vt), reinterpret_cast<f16*>(o), H, T,
+                     Tpad, ldo);
+  return hipGetLastError();
+}
+
 }  // namespace
 
 size_t attention_split_ws_bytes(int B, int H, int T) {
@@ -576,9 +825,10 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
   // cfg = <waves>[s<split>][g<groups>][r<ring>][q2] ("8", "4", "4s8", "8r3", ...):
   // a forced launch shape (mde_op_attention_cfg: tests, tuning)
   const char* forced = cfg && cfg[0] ? cfg : nullptr;
-  int nw = 0, split = 1, ring = ATTN_RING, qs2 = 0, groups = 1;
+  int nw = 0, split = 1, ring = ATTN_RING, qs2 = 0, groups = 1, m16 = 0;
   if (forced) {
     nw = atoi(forced);
+    m16 = strchr(forced, 'm') != nullptr;  // "<waves>m": the 16x16x32 kernel (attn16_fwd_kernel)
     const char* sp = strchr(forced, 's');
     split = sp ? atoi(sp + 1) : 1;
     const char* rp = strchr(forced, 'r');
@@ -615,6 +865,11 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
       split = 1;
       groups = 2;
     }
+  }
+  if (!forced && nw == 8 && groups == 1 && split <= 1) m16 = knob(KNOB_ATTN16);
+  if (m16 && groups == 1 && split <= 1 && !qs2) {
+    if (nw == 8) return run_attn16<8>(q, k, vt, o, B, H, T, Tpad, ldo, st);
+    if (nw == 4) return run_attn16<4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
   }
   if (groups > 1 && nkt >= groups) {
     if (nw == 4 && groups == 2) return run_attn_grp<4, 2>(q, k, vt, o, B, H, T, Tpad, ldo, st);

@@ -51,6 +51,10 @@ enum Knob : int {
   // 32 x 64 tiles with the whole K loop and a 4-deep ring instead of split-K
   // slices + the reduce launch (1: on).  test_narrow_resid_matches_split
   KNOB_NARROW_RESID,
+  // the large-grid attention (8 waves, unsplit: B = 48) on
+  // v_mfma_f32_16x16x32_f16 (attn16_fwd_kernel; 1: on; 0: the 32x32x16
+  // attn_fwd_kernel).  test_attention_16x16_matches
+  KNOB_ATTN16,
   KNOB_COUNT
 };
 

@@ -376,6 +376,47 @@ def test_attention_tuning_configs(gpu, cfg, B, H, T):
     close(o, ref, 2e-2, 5e-3, f"attention cfg {cfg} B{B} H{H} T{T}")
 
 
+@pytest.mark.parametrize("cfg", ["8m", "4m"])
+@pytest.mark.parametrize("B,H,T,spiky", [(2, 3, 300, False), (1, 6, 1370, True), (3, 5, 577, False), (1, 2, 20, False),
+                                         (16, 6, 1370, False), (1, 1, 1, False), (2, 2, 700, True)])
+def test_attention_16x16_matches(gpu, cfg, B, H, T, spiky):
+    """attn16_fwd_kernel (v_mfma_f32_16x16x32_f16, switch "attn16"): against
+    torch, with partial last blocks (T 300, 577, 20, 1), the rescale path
+    (spiky: dominant keys early and late), and -- the policy's switch -- the
+    default launch with attn16 = 1 bit-identical to the forced "8m" shape."""
+    Tp = -(-T // 64) * 64
+    q = rn(B * H, T, 64) * 0.125 * 2.0 * LOG2E
+    k = rn(B * H, T, 64) * 2.0
+    if spiky:
+        k[:, T - 10] = q.mean(1) * 60.0
+        k[:, 3] = q.mean(1) * 30.0
+    v = rn(B * H, T, 64)
+    ref = attn_ref(q, k, v).reshape(B, H, T, 64).permute(0, 2, 1, 3).reshape(B * T, H * 64)
+    qg = torch.zeros(B * H, Tp, 64, dtype=torch.float16, device=gpu)
+    kg = torch.zeros_like(qg)
+    vtg = torch.zeros(B * H, 64, Tp, dtype=torch.float16, device=gpu)
+    qg[:, :T], kg[:, :T] = q.half().to(gpu), k.half().to(gpu)
+    vtg[:, :, vt_perm(T).to(gpu)] = v.transpose(1, 2).half().to(gpu)
+    o = torch.full((B * T, H * 64), float("nan"), dtype=torch.float16, device=gpu)
+    op("mde_op_attention_cfg", ptr(qg), ptr(kg), ptr(vtg), ptr(o), B, H, T, Tp, H * 64, cfg.encode(), None, 0,
+       stream())
+    close(o, ref, 2e-2, 5e-3, f"attention {cfg} B{B} H{H} T{T}")
+    from monocular_depth_estimation_trt_amd import _lib
+    o32 = torch.empty_like(o)
+    with _lib.tuning(attn16=0):
+        op("mde_op_attention", ptr(qg), ptr(kg), ptr(vtg), ptr(o32), B, H, T, Tp, H * 64, stream())
+        torch.cuda.synchronize()
+    d = (o.float() - o32.float()).abs().max().item()
+    print(f"attention {cfg} B{B} H{H} T{T}: max |16x16 - 32x32| {d:.3g}")
+    if cfg == "8m" and (B * H * -(-T // 256)) >= 512:  # the policy picks 8 unsplit waves: the switch applies
+        with _lib.tuning(attn16=1):
+            o16 = torch.empty_like(o)
+            op("mde_op_attention", ptr(qg), ptr(kg), ptr(vtg), ptr(o16), B, H, T, Tp, H * 64, stream())
+            torch.cuda.synchronize()
+        assert torch.equal(o16, o), "attn16 = 1 default launch differs from the forced 8m shape"
+        assert not torch.equal(o32, o), "attn16 = 0 should launch the 32x32x16 kernel"
+
+
 def test_attention_spiky_rows(gpu):
     """Force the online-softmax rescale: one key dominates late in the row."""
     B, H, T = 1, 2, 300
