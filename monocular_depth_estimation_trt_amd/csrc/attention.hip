@@ -499,15 +499,16 @@ attn_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16*
 // P^T B operand of the P.V MFMA against the unchanged V^T layout (vt_pos).
 // The running max rides in the score C operand (one 4-register copy per
 // query sub-tile serves both key sub-tiles); a query's keys sit in four lane
-// groups, so the rare rescale's row max and the final row sum reduce with
-// v_permlane32_swap + v_permlane16_swap.
+// groups, so the rare rescale's row max reduces with v_permlane32_swap +
+// v_permlane16_swap; the row sums come from two more MFMAs with an all-ones
+// A operand (below).
 MDE_DEV int swz16(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
-MDE_DEV float grp4(float x, bool sum) {  // max / sum over lanes (l & 15) + 16 g, g = 0..3
+MDE_DEV float grp4_max(float x) {  // max over lanes (l & 15) + 16 g, g = 0..3
   auto a = __builtin_amdgcn_permlane32_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  x = sum ? __uint_as_float(a[0]) + __uint_as_float(a[1]) : fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
+  x = fmaxf(__uint_as_float(a[0]), __uint_as_float(a[1]));
   auto c = __builtin_amdgcn_permlane16_swap(__float_as_uint(x), __float_as_uint(x), false, false);
-  return sum ? __uint_as_float(c[0]) + __uint_as_float(c[1]) : fmaxf(__uint_as_float(c[0]), __uint_as_float(c[1]));
+  return fmaxf(__uint_as_float(c[0]), __uint_as_float(c[1]));
 }
 
 template <int NW>
@@ -559,11 +560,12 @@ attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f1
     }
   };
 
-  float m_run[2] = {0.f, 0.f}, l_run[2] = {0.f, 0.f};
-  f32x4 negm[2], acc[4][2];
+  float m_run[2] = {0.f, 0.f};
+  f32x4 negm[2], acc[4][2], lacc[2];  // lacc: the row sums, of the f16 P, by MFMA
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
     negm[s] = f32x4{0.f, 0.f, 0.f, 0.f};
+    lacc[s] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int dt = 0; dt < 4; ++dt) acc[dt][s] = f32x4{0.f, 0.f, 0.f, 0.f};
   }
@@ -616,7 +618,7 @@ attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f1
       mx = fmaxf(fmaxf(mx, sc.v[1][s][1]), sc.v[1][s][2]);
       mx = fmaxf(mx, sc.v[1][s][3]);
       if (FIRST || __any(mx > RESCALE_T)) {
-        mx = grp4(mx, false);  // the query's block max (relative to m_run)
+        mx = grp4_max(mx);  // the query's block max (relative to m_run)
         const float delta = FIRST ? mx : fmaxf(mx, 0.f);
         m_run[s] += delta;
         negm[s] = f32x4{-m_run[s], -m_run[s], -m_run[s], -m_run[s]};
@@ -624,7 +626,7 @@ attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f1
         sc.v[1][s] -= delta;
         if (!FIRST) {
           const float alpha = __builtin_amdgcn_exp2f(-delta);
-          l_run[s] *= alpha;
+          lacc[s] *= alpha;
 #pragma unroll
           for (int dt = 0; dt < 4; ++dt) acc[dt][s] *= alpha;
         }
@@ -638,16 +640,11 @@ attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f1
     Pb16 pb;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
-      float ls0, ls1;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        const float p0 = __builtin_amdgcn_exp2f(sc.v[0][s][r]), p1 = __builtin_amdgcn_exp2f(sc.v[1][s][r]);
-        ls0 = r ? ls0 + p0 : p0;
-        ls1 = r ? ls1 + p1 : p1;
-        pb.v[s][r] = (f16)p0;
-        pb.v[s][4 + r] = (f16)p1;
+        pb.v[s][r] = (f16)__builtin_amdgcn_exp2f(sc.v[0][s][r]);
+        pb.v[s][4 + r] = (f16)__builtin_amdgcn_exp2f(sc.v[1][s][r]);
       }
-      l_run[s] += ls0 + ls1;
     }
     return pb;
   };
@@ -659,6 +656,14 @@ attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f1
 #pragma unroll
       for (int s = 0; s < 2; ++s) acc[dt][s] = mfma16x16x32(vf, pb.v[s], acc[dt][s]);
     }
+    // row sums: an all-ones A operand makes every row of D the query's sum of
+    // its 32 f16 probabilities -- the same P the numerator used -- in place of
+    // 16 fp32 adds per lane and the final cross-lane sum (2 MFMAs, 16 cycles each)
+    f16x8 ones;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) ones[j] = (f16)1.0f;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) lacc[s] = mfma16x16x32(ones, pb.v[s], lacc[s]);
   };
   using NF = std::false_type;
   auto step = [&](int kt, auto slot_tag, auto first_tag) {
@@ -700,7 +705,7 @@ attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f1
   // exchange (v_permlane16_swap) so each lane stores 8 consecutive dh (16 B)
 #pragma unroll
   for (int s = 0; s < 2; ++s) {
-    const float inv = 1.f / grp4(l_run[s], true);
+    const float inv = 1.f / lacc[s][0];
     const int qs = qbase + 16 * s + l15;
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
