@@ -511,18 +511,28 @@ MDE_DEV float grp4_max(float x) {  // max over lanes (l & 15) + 16 g, g = 0..3
   return fmaxf(__uint_as_float(c[0]), __uint_as_float(c[1]));
 }
 
-template <int NW>
+// Per-lane floats one wave of a key group > 0 parks for the merge: O^T (32), m (2), l (2)
+constexpr int MERGE16_WAVE_B = 64 * 36 * 4;
+
+template <int NW, int NS>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4, 8)))
 attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16* __restrict__ vt,
                   f16* __restrict__ o, int H, int T, int Tpad, int ldo) {
-  static_assert(NW == 4 || NW == 8, "waves per workgroup");
-  constexpr int BQ = QW * NW;
-  constexpr int INS = 8 / NW;  // glds row groups per wave per 64-row image
-  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
+  // NS > 1 (batch-1 grids): NS key groups of NW / NS query waves, as in
+  // attn_fwd_kernel -- each group streams its slice of the key tiles through
+  // its own ring slots, (O, m, l) merged through LDS after the loop
+  constexpr int NWQ = NW / NS;  // query waves per key group
+  static_assert(NWQ * NS == NW && (NWQ == 2 || NWQ == 4 || NWQ == 8) && (NW == 4 || NW == 8), "waves");
+  constexpr int BQ = QW * NWQ;
+  constexpr int INS = 8 / NWQ;  // glds row groups per wave per 64-row image
+  constexpr int RING_B = 2 * NS * SLOT, MERGE_B = (NS - 1) * NWQ * MERGE16_WAVE_B;
+  __shared__ __attribute__((aligned(16))) char smem[RING_B > MERGE_B ? RING_B : MERGE_B];
 
   const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  if (NW == 8 && wave >= 4) __builtin_amdgcn_s_setprio(1);
+  const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = NS > 1 ? wave_all / NWQ : 0;
+  const int wave = wave_all - grp * NWQ;
+  if (NW == 8 && NS == 1 && wave_all >= 4) __builtin_amdgcn_s_setprio(1);
   const int nqb = gridDim.x;
   const int lin = xcd_remap(blockIdx.y * nqb + blockIdx.x, nqb * gridDim.y);
   const int bh = lin / nqb;
@@ -530,7 +540,9 @@ attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f1
   const int qbase = (lin - bh * nqb) * BQ + wave * QW;
   const bool active = qbase < T;
   const int l15 = lane & 15, g = lane >> 4;
-  const int nkt = (T + KT - 1) / KT;
+  const int nkt_all = (T + KT - 1) / KT;
+  const int gper = (nkt_all + NS - 1) / NS;  // key tiles per group
+  const int kt0 = grp * gper, kt1 = min(nkt_all, kt0 + gper), ktl = kt0 + gper;
 
   const f16* qb = q + (size_t)bh * Tpad * 64;
   const f16* kb = k + (size_t)bh * Tpad * 64;
@@ -547,12 +559,13 @@ attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f1
   }
 
   const int lrow = lane >> 3, pc = lane & 7;
+  char* const gsm = smem + grp * SLOT;  // this key group's share of each ring slot
   auto issue = [&](int kt, int slot) {
-    char* sK = smem + slot * SLOT;
+    char* sK = gsm + slot * NS * SLOT;
     char* sV = sK + TILE_B;
 #pragma unroll
     for (int i = 0; i < INS; ++i) {
-      const int gg = wave + i * NW;  // 8-row group
+      const int gg = wave + i * NWQ;  // 8-row group
       const int row = gg * 8 + lrow;
       const int lc = pc ^ lrow;      // swz16: row & 7 == lrow
       __builtin_amdgcn_global_load_lds(kb + (size_t)(kt * KT + row) * 64 + lc * 8, sK + gg * 8 * 128, 16, 0, 0);
@@ -668,9 +681,9 @@ attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f1
   using NF = std::false_type;
   auto step = [&](int kt, auto slot_tag, auto first_tag) {
     constexpr int SL = decltype(slot_tag)::value;
-    if (kt + 1 < nkt) issue(kt + 1, SL ^ 1);  // into the slot of tile kt - 1 (released by the last barrier)
-    if (active) {
-      const char* K_ = smem + SL * SLOT;
+    if (kt + 1 < kt1) issue(kt + 1, SL ^ 1);  // into the slot of tile kt - 1 (released by the last barrier)
+    if (active && kt < kt1) {
+      const char* K_ = gsm + SL * NS * SLOT;
       Sc16 s0 = scores(K_, kt, 0, first_tag);
       mask(s0, kt, 0);
       rescale(s0, first_tag);
@@ -689,16 +702,53 @@ attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f1
   };
   using S0 = std::integral_constant<int, 0>;
   using S1 = std::integral_constant<int, 1>;
-  issue(0, 0);
+  if (kt0 < kt1) issue(kt0, 0);
   wait_vm_n<0>();
   lds_barrier();
-  step(0, S0{}, std::true_type{});
-  int kt = 1;
-  for (; kt + 2 <= nkt; kt += 2) {
+  step(kt0, S0{}, std::true_type{});
+  int kt = kt0 + 1;
+  for (; kt + 2 <= ktl; kt += 2) {
     step(kt, S1{}, NF{});
     step(kt + 1, S0{}, NF{});
   }
-  if (kt < nkt) step(kt, S1{}, NF{});
+  if (kt < ktl) step(kt, S1{}, NF{});
+
+  if constexpr (NS > 1) {
+    // merge: groups 1.. park (O^T, m, l) in LDS (the ring is free: the last
+    // step waited out every load and its barrier every read), group 0
+    // rescales to the common max and sums; lane layouts match across groups
+    float* mb = reinterpret_cast<float*>(smem);
+    if (grp > 0) {
+      float* w = mb + ((grp - 1) * NWQ + wave) * (MERGE16_WAVE_B / 4);
+#pragma unroll
+      for (int c = 0; c < 8; ++c) *reinterpret_cast<f32x4*>(w + (c * 64 + lane) * 4) = acc[c >> 1][c & 1];
+      *reinterpret_cast<f32x4*>(w + 8 * 64 * 4 + lane * 4) = f32x4{m_run[0], m_run[1], lacc[0][0], lacc[1][0]};
+    }
+    __syncthreads();
+    if (grp > 0) return;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      float mmax = m_run[s];
+#pragma unroll
+      for (int gr = 1; gr < NS; ++gr)
+        if (gr * gper < nkt_all)
+          mmax = fmaxf(mmax, mb[((gr - 1) * NWQ + wave) * (MERGE16_WAVE_B / 4) + 8 * 64 * 4 + lane * 4 + s]);
+      const float a0 = __builtin_amdgcn_exp2f(m_run[s] - mmax);
+      lacc[s] *= a0;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) acc[dt][s] *= a0;
+#pragma unroll
+      for (int gr = 1; gr < NS; ++gr) {
+        if (gr * gper >= nkt_all) continue;  // an empty group (tiny T)
+        const float* w = mb + ((gr - 1) * NWQ + wave) * (MERGE16_WAVE_B / 4);
+        const f32x4 ml = *reinterpret_cast<const f32x4*>(w + 8 * 64 * 4 + lane * 4);
+        const float ag = __builtin_amdgcn_exp2f(ml[s] - mmax);
+        lacc[s][0] += ag * ml[2 + s];
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) acc[dt][s] += ag * *reinterpret_cast<const f32x4*>(w + ((2 * dt + s) * 64 + lane) * 4);
+      }
+    }
+  }
   if (!active) return;
 
   // epilogue: lane holds O^T[16 dt + 4 g + r][16 s + l15]; lane groups g, g ^ 1
@@ -803,11 +853,12 @@ hipError_t run_attn_grp(const h16* q, const h16* k, const h16* vt, h16* o, int B
   return hipGetLastError();
 }
 
-template <int NW>
+template <int NW, int NS = 1>
 hipError_t run_attn16(const h16* q, const h16* k, const h16* vt, h16* o, int B, int H, int T, int Tpad, int ldo,
                       hipStream_t st) {
-  const int nqb = (T + QW * NW - 1) / (QW * NW);
-  hipLaunchKernelGGL((attn16_fwd_kernel<NW>), dim3(nqb, B * H), dim3(NW * 64), 0, st, reinterpret_cast<const f16*>(q),
+  constexpr int BQ = QW * (NW / NS);
+  const int nqb = (T + BQ - 1) / BQ;
+  hipLaunchKernelGGL((attn16_fwd_kernel<NW, NS>), dim3(nqb, B * H), dim3(NW * 64), 0, st, reinterpret_cast<const f16*>(q),
                      reinterpret_cast<const f16*>(k), reinterpret_cast<const f16*>(vt), reinterpret_cast<f16*>(o), H, T,
                      Tpad, ldo);
   return hipGetLastError();
@@ -871,7 +922,14 @@ hipError_t launch_attention(const h16* q, const h16* k, const h16* vt, h16* o, i
       groups = 2;
     }
   }
+  // (the key-group form, cfg "8g2m" / "8g4m", measured 3 % slower than the
+  // 32x32x16 one at batch 1: ViT-L 17.4-17.9 vs 16.9-17.4 us, ViT-S 12.4-12.7
+  // vs 12.1-12.4, gpurun_out r6s24 -- the switch covers the unsplit shape only)
   if (!forced && nw == 8 && groups == 1 && split <= 1) m16 = knob(KNOB_ATTN16);
+  if (m16 && groups > 1 && nkt >= groups && nw == 8 && split <= 1 && !qs2) {
+    if (groups == 2) return run_attn16<8, 2>(q, k, vt, o, B, H, T, Tpad, ldo, st);
+    if (groups == 4) return run_attn16<8, 4>(q, k, vt, o, B, H, T, Tpad, ldo, st);
+  }
   if (m16 && groups == 1 && split <= 1 && !qs2) {
     if (nw == 8) return run_attn16<8>(q, k, vt, o, B, H, T, Tpad, ldo, st);
     if (nw == 4) return run_attn16<4>(q, k, vt, o, B, H, T, Tpad, ldo, st);

@@ -323,7 +323,7 @@ def test_attention_split_kv(gpu, B, H, T, spiky):
     close(o, ref, 2e-2, 5e-3, f"attention split-KV B{B} H{H} T{T}")
 
 
-@pytest.mark.parametrize("cfg", ["4g2", "8g2", "4g4", "8g4", "12g3", "16g4", "6g2"])
+@pytest.mark.parametrize("cfg", ["4g2", "8g2", "4g4", "8g4", "12g3", "16g4", "6g2", "8g2m", "8g4m"])
 @pytest.mark.parametrize("B,H,T,spiky", [(1, 16, 1370, False), (1, 6, 1370, True), (2, 3, 129, False),
                                          (1, 2, 300, True), (1, 1, 200, False)])
 def test_attention_key_groups(gpu, cfg, B, H, T, spiky):
