@@ -622,7 +622,12 @@ attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f1
   };
   // online softmax of one block's scores: the running max (rescale when it
   // grows past RESCALE_T), then P = exp2(S') as the P.V B operand and the row sums
-  auto rescale = [&](Sc16& sc, auto first_tag) {
+  struct Pb16 {
+    f16x8 v[2];
+  };
+  // pend: probabilities computed against the old max whose P.V is still to
+  // come (block 0's, issued under block 1's exp2 chain) -- scaled with O
+  auto rescale = [&](Sc16& sc, auto first_tag, Pb16* pend) {
     constexpr bool FIRST = decltype(first_tag)::value;
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
@@ -642,12 +647,14 @@ attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f1
           lacc[s] *= alpha;
 #pragma unroll
           for (int dt = 0; dt < 4; ++dt) acc[dt][s] *= alpha;
+          if (pend) {
+            const f16 ah = (f16)alpha;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) pend->v[s][j] *= ah;
+          }
         }
       }
     }
-  };
-  struct Pb16 {
-    f16x8 v[2];
   };
   auto probs = [&](const Sc16& sc) {
     Pb16 pb;
@@ -682,20 +689,23 @@ attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f1
   auto step = [&](int kt, auto slot_tag, auto first_tag) {
     constexpr int SL = decltype(slot_tag)::value;
     if (kt + 1 < kt1) issue(kt + 1, SL ^ 1);  // into the slot of tile kt - 1 (released by the last barrier)
+    // two overlapped phases per tile: block 1's score MFMAs (against the
+    // updated max) beside block 0's exp2 chain, then block 0's P.V MFMAs
+    // beside block 1's exp2 chain (a rescale in between scales block 0's
+    // pending P with O).  (A copy of the tile body without the masking
+    // branches for the full tiles measured no faster, r6s25.)
     if (active && kt < kt1) {
       const char* K_ = gsm + SL * NS * SLOT;
       Sc16 s0 = scores(K_, kt, 0, first_tag);
       mask(s0, kt, 0);
-      rescale(s0, first_tag);
-      // block 1's score MFMAs (against the updated max) are independent of
-      // block 0's exp2 chain: with the masking branch moved after them, hipcc
-      // interleaves the two (one MFMA per 3-4 VALU)
+      rescale(s0, first_tag, nullptr);
       Sc16 s1 = scores(K_, kt, 1, NF{});
-      const Pb16 p0 = probs(s0);
-      pv(p0, K_ + TILE_B, 0);
       mask(s1, kt, 1);
-      rescale(s1, NF{});
-      pv(probs(s1), K_ + TILE_B, 1);
+      Pb16 p0 = probs(s0);
+      rescale(s1, NF{}, &p0);
+      pv(p0, K_ + TILE_B, 0);
+      const Pb16 p1 = probs(s1);
+      pv(p1, K_ + TILE_B, 1);
     }
     wait_vm_n<0>();
     lds_barrier();
