@@ -31,7 +31,7 @@ def test_attention_hot_loop_valu_per_mfma():
 
 @pytest.mark.skipif(not (shutil.which("hipcc") or os.path.exists("/opt/rocm/bin/hipcc")), reason="hipcc absent")
 def test_attention16_hot_loop_census():
-    """The default B = 48 kernel since round 6 (attn16_fwd_kernel<8>, switch
+    """The default B = 48 kernel since round 6 (attn16_fwd_kernel<8, 1>, switch
     "attn16"): per 32-key block 18 v_mfma_f32_16x16x32_f16 (8 score, 8 P.V,
     2 row sums against an all-ones operand) and the softmax's 16 exp2 -- 8/9
     transcendental per MFMA -- with no fp32 row-sum adds left; the census
@@ -41,7 +41,7 @@ def test_attention16_hot_loop_census():
     import isa_census
     dis = isa_census.disassemble(os.path.join(ROOT, "monocular_depth_estimation_trt_amd", "csrc", "attention.hip"))
     ks = isa_census.kernels(dis)
-    name = next(k for k in ks if "attn16_fwd_kernelILi8EE" in k)
+    name = next(k for k in ks if "attn16_fwd_kernelILi8ELi1EE" in k)
     hot = isa_census.analyse(ks[name])["hot_path"]
     assert hot["classes"]["mfma"] % 18 == 0 and hot["classes"]["mfma"] >= 36, hot
     assert hot["valu_per_mfma"] <= 3.0, hot
