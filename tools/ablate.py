@@ -62,6 +62,24 @@ VARIANTS = {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }""", """MDE_DEV void wait_vm_n() {
 }""", 1)]),
+    # attn16 (16x16x32 attention): the exponentials replaced by their argument
+    "a16_noexp": ("attention.hip", [
+        ("pb.v[s][r] = (f16)__builtin_amdgcn_exp2f(sc.v[0][s][r]);\n        pb.v[s][4 + r] = (f16)__builtin_amdgcn_exp2f(sc.v[1][s][r]);",
+         "pb.v[s][r] = (f16)sc.v[0][s][r];\n        pb.v[s][4 + r] = (f16)sc.v[1][s][r];", 1)]),
+    # attn16: no P.V / row-sum MFMAs (operands kept live)
+    "a16_nopv": ("attention.hip", [
+        ("for (int s = 0; s < 2; ++s) acc[dt][s] = mfma16x16x32(vf, pb.v[s], acc[dt][s]);",
+         'for (int s = 0; s < 2; ++s) asm volatile("" :: "v"(vf), "v"(pb.v[s]));', 1),
+        ("for (int s = 0; s < 2; ++s) lacc[s] = mfma16x16x32(ones, pb.v[s], lacc[s]);",
+         'for (int s = 0; s < 2; ++s) asm volatile("" :: "v"(ones), "v"(pb.v[s]));', 1)]),
+    # attn16: no score MFMAs (K fragments kept live, scores = C operand)
+    "a16_noqk": ("attention.hip", [
+        ("for (int s = 0; s < 2; ++s) sc.v[t][s] = mfma16x16x32(kf, qf[s][d], sc.v[t][s]);",
+         'for (int s = 0; s < 2; ++s) asm volatile("" :: "v"(kf), "v"(qf[s][d]));', 1)]),
+    # attn16: no rescale check (the running max never moves after the first block)
+    "a16_nomax": ("attention.hip", [
+        ("      if (FIRST || __any(mx > RESCALE_T)) {\n        mx = grp4_max(mx);",
+         '      asm volatile("" :: "v"(mx));\n      if (FIRST) {\n        mx = grp4_max(mx);', 1)]),
     # candidate (not an ablation): batch-1 stores / qkv whose 128^2 grid
     # overhangs the CUs by a partial round (ViT-L B=1 qkv 264, fc1 352 tiles)
     # on 256 x 128 tiles (8 waves of 64 x 64, BK 32 x 3 stages, two per CU):
