@@ -80,6 +80,18 @@ VARIANTS = {
     "a16_nomax": ("attention.hip", [
         ("      if (FIRST || __any(mx > RESCALE_T)) {\n        mx = grp4_max(mx);",
          '      asm volatile("" :: "v"(mx));\n      if (FIRST) {\n        mx = grp4_max(mx);', 1)]),
+    # attention (both kernels): no static priority for waves 4-7
+    "attn_noprio": ("attention.hip", [
+        ("if (NW == 8 && NS == 1 && wave_all >= 4) __builtin_amdgcn_s_setprio(1);", "", 2)]),
+    # attention (both kernels): the static priority on waves 0-3 instead
+    "attn_prio_lo": ("attention.hip", [
+        ("if (NW == 8 && NS == 1 && wave_all >= 4) __builtin_amdgcn_s_setprio(1);",
+         "if (NW == 8 && NS == 1 && wave_all < 4) __builtin_amdgcn_s_setprio(1);", 2)]),
+    # attention (both kernels): priority 2 / 1 / 0 by wave pair (waves 6-7, 4-5, rest)
+    "attn_prio3": ("attention.hip", [
+        ("if (NW == 8 && NS == 1 && wave_all >= 4) __builtin_amdgcn_s_setprio(1);",
+         "if (NW == 8 && NS == 1 && wave_all >= 6) __builtin_amdgcn_s_setprio(2); "
+         "else if (NW == 8 && NS == 1 && wave_all >= 4) __builtin_amdgcn_s_setprio(1);", 2)]),
     # candidate (not an ablation): batch-1 stores / qkv whose 128^2 grid
     # overhangs the CUs by a partial round (ViT-L B=1 qkv 264, fc1 352 tiles)
     # on 256 x 128 tiles (8 waves of 64 x 64, BK 32 x 3 stages, two per CU):
