@@ -64,16 +64,32 @@ MFMA_PEAK_TFLOPS = 2500.0   # dense fp16/bf16 MFMA, MI355X spec (MI355X_MICROARC
 MFMA_PEAK_FILE = os.path.join(ROOT, "profiles", "r03_mfma_peak.json")
 
 
-def measured_peak(kernel_class: str):
+def measured_peak(kernel_class: str, attn16: bool = False):
     """(TFLOP/s, MFMA shape) the chip sustains for the instruction the class's
-    kernel issues, from the committed microbenchmark; (None, None) without it."""
+    kernel issues, from the committed microbenchmark; (None, None) without it.
+    attn16: the attention launch is attn16_fwd_kernel (16x16x32, round 6)."""
     try:
         with open(MFMA_PEAK_FILE) as f:
             d = json.load(f)
     except (OSError, ValueError):
         return None, None
-    shape = "32x32x16" if kernel_class.split(".")[-1] in ("attn", "attention", "gattn", "fattn") else "16x16x32"
+    is_attn = kernel_class.split(".")[-1] in ("attn", "attention", "gattn", "fattn")
+    shape = "32x32x16" if is_attn and not attn16 else "16x16x32"
     return d.get(f"mfma_f16_{shape}_tflops"), shape
+
+
+def attn16_active(cfg, B, size) -> bool:
+    """Whether the DA-V2 attention launches run attn16_fwd_kernel: switch
+    "attn16" on and the launcher's 8-wave unsplit shape (attention.hip
+    launch_attention: B * heads * ceil(T / 256) >= 512)."""
+    if cfg.get("family") in ("depth_pro", "vggt"):
+        return False
+    from monocular_depth_estimation_trt_amd import _lib
+    if _lib.get_tuning("attn16") != 1:
+        return False
+    h, w = size if isinstance(size, tuple) else (size, size)
+    T = (h // cfg["patch"]) * (w // cfg["patch"]) + 1
+    return B * int(cfg["num_heads"]) * -(-T // 256) >= 512
 ENC_LABEL = {"vits": "ViT-S", "vitb": "ViT-B", "vitl": "ViT-L"}
 REF_B1_FPS = 232.11         # RTX 3080 TRT fp16, BASELINE.md
 REF_B1_FP32_FPS = 88.29     # RTX 3080 TRT fp32 (the reference's default build), reports/tune/fp32_depth_anything_v2.json
@@ -200,7 +216,7 @@ def roofline(cfg, B, size, layer_ms, frames=1, traffic_file=""):
             "unit": "TFLOP/s", "frac": round(achieved / MFMA_PEAK_TFLOPS, 4), "traffic": traffic,
             "flop_per_launch": per_launch_fl, "avg_launch_ms": round(avg_ms, 5),
             "launches_per_step": cls_n[dom]}
-    mp, shape = measured_peak(dom)
+    mp, shape = measured_peak(dom, attn16_active(cfg, B, size))
     if mp:
         roof.update({"peak_source": "spec (MI355X_MICROARCH.md)", "peak_measured": mp,
                      "peak_measured_mfma": f"v_mfma_f32_{shape}_f16",

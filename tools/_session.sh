@@ -1,8 +1,10 @@
 set -o pipefail
-O=gpurun_out/r6s26
+O=gpurun_out/r6ev2b
 mkdir -p $O
-for it in 1 2; do
-  for L in monocular_depth_estimation_trt_amd/libmde_hip.so build/var/lib_a16_noexp.so build/var/lib_a16_nopv.so build/var/lib_a16_noqk.so build/var/lib_a16_nomax.so build/var/lib_attn_nosync.so; do
-    timeout -k 10 120 python tools/bench_kernels.py --lib $L --batch 48 --iters 40 --only attention --attn-cfgs 8m,8m > $O/kern_$(basename $L .so)_$it.log 2>&1 || exit 1
-  done
-done
+bash tools/gpu_tasks.sh $O bench:def: \
+  bench:vitl1:--encoder,vitl,--batch,1,--no-cpu-baseline,--no-pcie \
+  bench:fp32:--precision,fp32,--batch,8,--no-cpu-baseline,--no-pcie \
+  bench:s392:--size,392x518,--no-cpu-baseline,--no-pcie \
+  bench:s672:--size,672x896,--no-cpu-baseline,--no-pcie \
+  bench:dp:--model,depth_pro,--no-cpu-baseline,--no-pcie \
+  bench:vggt:--model,vggt,--no-cpu-baseline,--no-pcie || exit 1
