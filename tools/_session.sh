@@ -1,10 +1,9 @@
 set -o pipefail
-O=gpurun_out/r6ev2b
+O=gpurun_out/r6s29
 mkdir -p $O
-bash tools/gpu_tasks.sh $O bench:def: \
-  bench:vitl1:--encoder,vitl,--batch,1,--no-cpu-baseline,--no-pcie \
-  bench:fp32:--precision,fp32,--batch,8,--no-cpu-baseline,--no-pcie \
-  bench:s392:--size,392x518,--no-cpu-baseline,--no-pcie \
-  bench:s672:--size,672x896,--no-cpu-baseline,--no-pcie \
-  bench:dp:--model,depth_pro,--no-cpu-baseline,--no-pcie \
-  bench:vggt:--model,vggt,--no-cpu-baseline,--no-pcie || exit 1
+for it in 1 2; do
+  for L in monocular_depth_estimation_trt_amd/libmde_hip.so build/var/lib_uc_nov.so build/var/lib_uc_noh.so build/var/lib_uc_nomfma.so; do
+    n=$(basename $L .so)
+    timeout -k 10 300 python -u tools/bench_lib.py $L --steps 10 --no-b1 --no-cpu-baseline --no-pcie --profile-iters 5 --layers-json $O/layers_${n}_$it.json > $O/bench_${n}_$it.json 2> $O/bench_${n}_$it.err || exit 1
+  done
+done

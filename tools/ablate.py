@@ -92,6 +92,20 @@ VARIANTS = {
         ("if (NW == 8 && NS == 1 && wave_all >= 4) __builtin_amdgcn_s_setprio(1);",
          "if (NW == 8 && NS == 1 && wave_all >= 6) __builtin_amdgcn_s_setprio(2); "
          "else if (NW == 8 && NS == 1 && wave_all >= 4) __builtin_amdgcn_s_setprio(1);", 2)]),
+    # separable upsampling conv: pass V reduced to its patch stores (no row index math, H reads, lerp)
+    "uc_nov": ("conv.hip", [
+        ("""        f16x8 v = zero8();
+        if (xin && iy >= 0 && iy < p.uh) {
+          int y0, y1;""", """        f16x8 v = zero8();
+        if (false) {
+          int y0, y1;""", 1)]),
+    # separable upsampling conv: pass H commits one source column (no lerp)
+    "uc_noh": ("conv.hip", [
+        ("hin ? lerp8(ha[k], hb[k], hw) : zero8();", "ha[k];", 1)]),
+    # separable upsampling conv: no tap MFMAs (fragments kept live)
+    "uc_nomfma": ("conv.hip", [
+        ("          for (int j = 0; j < TN; ++j) acc[i][j] = mfma16x16x32(fb[j], fa[i], acc[i][j]);\n        if constexpr (PERSIST)",
+         '          for (int j = 0; j < TN; ++j) asm volatile("" :: "v"(fb[j]), "v"(fa[i]));\n        if constexpr (PERSIST)', 1)]),
     # candidate (not an ablation): batch-1 stores / qkv whose 128^2 grid
     # overhangs the CUs by a partial round (ViT-L B=1 qkv 264, fc1 352 tiles)
     # on 256 x 128 tiles (8 waves of 64 x 64, BK 32 x 3 stages, two per CU):
