@@ -417,6 +417,32 @@ def test_attention_16x16_matches(gpu, cfg, B, H, T, spiky):
         assert not torch.equal(o32, o), "attn16 = 0 should launch the 32x32x16 kernel"
 
 
+@pytest.mark.parametrize("cfg", ["8m", "8g2m"])
+def test_attention_16x16_pending_rescale(gpu, cfg):
+    """attn16 scores a tile's second 32-key block before block 0's P.V; when
+    block 1 moves the running max, block 0's pending f16 P is scaled with O
+    (attention.hip rescale(..., pend)).  Dominant keys only in second blocks
+    (key % 64 >= 32: 50, 120, 250), each larger than the last, force that path
+    in the first tile (after the FIRST block), a middle and the last tile."""
+    B, H, T = 2, 3, 300
+    Tp = -(-T // 64) * 64
+    q = rn(B * H, T, 64) * 0.125 * 2.0 * LOG2E
+    k = rn(B * H, T, 64) * 2.0
+    for key, mag in ((50, 20.0), (120, 40.0), (250, 80.0)):
+        k[:, key] = q.mean(1) * mag
+    v = rn(B * H, T, 64)
+    ref = attn_ref(q, k, v).reshape(B, H, T, 64).permute(0, 2, 1, 3).reshape(B * T, H * 64)
+    qg = torch.zeros(B * H, Tp, 64, dtype=torch.float16, device=gpu)
+    kg = torch.zeros_like(qg)
+    vtg = torch.zeros(B * H, 64, Tp, dtype=torch.float16, device=gpu)
+    qg[:, :T], kg[:, :T] = q.half().to(gpu), k.half().to(gpu)
+    vtg[:, :, vt_perm(T).to(gpu)] = v.transpose(1, 2).half().to(gpu)
+    o = torch.full((B * T, H * 64), float("nan"), dtype=torch.float16, device=gpu)
+    op("mde_op_attention_cfg", ptr(qg), ptr(kg), ptr(vtg), ptr(o), B, H, T, Tp, H * 64, cfg.encode(), None, 0,
+       stream())
+    close(o, ref, 2e-2, 5e-3, f"attention {cfg} pending-P rescale")
+
+
 def test_attention_spiky_rows(gpu):
     """Force the online-softmax rescale: one key dominates late in the row."""
     B, H, T = 1, 2, 300
