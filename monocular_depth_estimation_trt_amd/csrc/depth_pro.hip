@@ -176,7 +176,7 @@ size_t plan_arena_dp(const mde_engine& e, int B, DPBuf* b, uint8_t* base) {
     t.fv2 = a.h(bb * (GG / 4) * (F / 4));
     t.fv3 = a.h(bb * (GG / 16) * (F / 8));
   }
-  t.sws = a.f(kSplitWsFloats);
+  t.sws = a.f(kSplitWsAlloc);
   if (b) *b = t;
   return a.off;
 }

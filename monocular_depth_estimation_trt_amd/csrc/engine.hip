@@ -262,13 +262,13 @@ size_t plan_arena_dav2(const mde_engine& e, int B, DAV2Buf* b, uint8_t* base) {
     t.up2_32 = a.f(bb * sout * (F / 2));
     t.hid32 = a.f(bb * sout * 32);
   }
-  t.ws = h16enc && bb * e.T <= 4096 ? a.f(4 * bb * e.T * D) : nullptr;
+  t.ws = h16enc && bb * e.T <= 4096 ? a.f(fc2_ws_floats(bb * e.T, D)) : nullptr;
   // attention split-KV workspace for the batches whose (head, 128-query)
   // grid is under one workgroup per CU (launch_attention splits those)
   const int bsplit = std::min<int>(B, (256 + ((e.T + 127) / 128) * e.H - 1) / (((e.T + 127) / 128) * e.H));
   t.aws_bytes = h16enc && bsplit >= 1 ? attention_split_ws_bytes(bsplit, e.H, e.T) : 0;
   t.aws = t.aws_bytes ? a.f(t.aws_bytes / sizeof(float)) : nullptr;
-  t.sws = a.f(kSplitWsFloats);
+  t.sws = a.f(kSplitWsAlloc);
   if (b) *b = t;
   return a.off;
 }
@@ -609,6 +609,9 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
       if (b.ws && t64 < 512 && K >= 1024 && knob(KNOB_SPLITK)) {
         g.partial = b.ws;
         g.splitk = t64 < 256 ? 4 : 2;
+        g.slot_cap = fc2_ws_floats((size_t)B * T, D);
+        g.tile_cnt = split_counters(b.sws);
+        g.tile_cnt_cap = kTileCnt;
       }
     };
     // LayerNorm folded across the GEMM boundary (packs with folded weights):

@@ -53,6 +53,16 @@ struct DAV2Buf {
 // fp32 elements of a context's E_STORE split-K workspace (launch_gemm bounds
 // slices x M x N by it; the largest split the policy picks is ~4.2 M)
 constexpr size_t kSplitWsFloats = size_t(5) << 20;
+// the allocation behind it: the fused split-K slots are whole 64^2 tiles
+// (padding beyond M x N), then kTileCnt arrival counters (int, zeroed with the
+// arena; GemmParams::tile_cnt)
+constexpr size_t kSplitSlotFloats = size_t(6) << 20;
+constexpr int kTileCnt = 16384;
+constexpr size_t kSplitWsAlloc = kSplitSlotFloats + kTileCnt;
+inline int* split_counters(float* sws) { return sws ? reinterpret_cast<int*>(sws + kSplitSlotFloats) : nullptr; }
+// fc2 split-K partials of a small-batch context: [4][rows rounded up to 128][D]
+// (the fused form's 128^2 slots of D % 128 == 0 encoders fit)
+inline size_t fc2_ws_floats(size_t rows, int D) { return 4 * align_up(rows, 128) * (size_t)D; }
 
 // Depth Pro activations (depth_pro.hip plan_arena_dp).  Token buffers are
 // sized for the patch encoder (35 sequences per image), the largest of the
@@ -339,6 +349,9 @@ struct Runner {
     if (split_ws && g.emode == E_STORE && !g.partial) {
       q.partial = split_ws;
       q.partial_cap = kSplitWsFloats;
+      q.slot_cap = kSplitSlotFloats;
+      q.tile_cnt = split_counters(split_ws);
+      q.tile_cnt_cap = kTileCnt;
     }
     step(name, [&] { return launch_gemm(q, st); });
   }

@@ -112,7 +112,10 @@ struct KGeo {
 // workgroup's epilogue stores overlap the others' main loops
 // STG > 0: ring depth forced (small grids: one workgroup per CU with
 // STG - 1 K-steps in flight instead of two workgroups with one each)
-template <int BM, int BN, int BK, int WM, int WN, int AM, int EM, int STG = 0>
+// SPLIT: the fused split-K form (E_RESID / E_STORE over gridDim.y slices, the
+// tail after the main loop) -- separate instantiations, so the whole-tile
+// kernels carry none of its code or registers
+template <int BM, int BN, int BK, int WM, int WN, int AM, int EM, int STG = 0, bool SPLIT = false>
 __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
     __attribute__((amdgpu_waves_per_eu(STG == 0 && BK == 32 ? (WM * WN == 8 ? 4 : (MDE_BK32_STAGES > 2 ? 3 : 4)) : 1)))
     gemm_kernel(const GemmParams p) {
@@ -141,6 +144,10 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
   // folded LayerNorm consumers: (mean, var) of the tile's rows behind the ring
   constexpr bool LNF = AM == A_DENSE && (EM == E_QKV || EM == E_STORE);
   constexpr int LNB = LNF ? BM * 8 : 0;
+  // fused split-K: E_RESID / E_STORE launched with gridDim.y = S > 1 slices
+  // (the split tail after the main loop; gridDim.y = 1 is the plain tile)
+  constexpr bool FSPLIT = SPLIT && (EM == E_RESID || EM == E_STORE) && AM != A_CONV3_UP;
+  static_assert(!SPLIT || FSPLIT, "fused split-K: E_RESID / E_STORE over dense or im2col A");
   __shared__ __attribute__((aligned(16))) char smem[SG * STAGE + LNB];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -152,7 +159,7 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
   // (tn fastest) -- the N-tiles of one row block then share A in one L2.
   // Bijective for any grid size (cdna_hip_programming.md section 5).
   int bid = blockIdx.x, slice = blockIdx.y;
-  if constexpr (EM == E_PARTIAL) {
+  if constexpr (EM == E_PARTIAL || FSPLIT) {  // (gridDim.y = 1: the same order as below)
     // split-K: remap over (slice, tile) so each XCD takes a contiguous run of
     // one slice's tiles -- its L2 then holds that K-slice of W and of the A
     // rows, not every slice of both (a slice-blind order streams all of W
@@ -224,7 +231,7 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
   }
   // K-tiles [kt0, kt0 + nk): all of K, or this workgroup's split-K slice
   int nk = (p.K + BK - 1) / BK, kt0 = 0;
-  if constexpr (EM == E_PARTIAL) {
+  if constexpr (EM == E_PARTIAL || FSPLIT) {
     const int per = (nk + (int)gridDim.y - 1) / (int)gridDim.y;
     kt0 = slice * per;
     nk = min(nk - kt0, per);  // >= 1: the launcher uses at most nk slices of ceil(nk / S) tiles
@@ -432,6 +439,85 @@ __global__ void __launch_bounds__(WM * WN * 64) MDE_GEMM_WPE_ATTR
       lds_barrier();  // stage kt visible to all waves; stage kt-1 fully consumed
       if (kt + SG - 1 < nk) issue(kt + SG - 1, (kt + SG - 1) % SG);
       mma_stage(kt % SG);
+    }
+  }
+
+  // ---- fused split-K tail (gridDim.y = S > 1): each slice publishes its
+  // fp32 accumulators to its slot of p.partial in register order (16-B words
+  // thread-major per 16x16 block: coalesced), then bumps the tile's arrival
+  // counter p.tile_cnt[bid].  The LAST of the S slices to arrive adds the
+  // slots in slice order 0..S-1 -- the order of the reduce kernels, so the
+  // sum does not depend on which slice arrives last -- re-zeroes the counter
+  // for the next launch and runs the tile's own epilogue; the others exit.
+  // No workgroup ever waits on another.  The slices of a tile sit on
+  // different XCDs (slice-aware order above), so slots and counter go
+  // through system-scope (sc0 sc1) accesses that bypass the per-XCD L2s
+  // instead of a cache-wide __threadfence() write-back per slice.
+  if constexpr (FSPLIT) {
+    const int S = (int)gridDim.y;
+    if (S > 1) {
+      constexpr int NB = TM * TN;
+      typedef unsigned long long u64;
+      u64* const slots = reinterpret_cast<u64*>(p.partial);
+      const size_t slot_words = (size_t)NB * NT * 2;
+      auto word = [&](int s, int blk) {
+        return slots + ((size_t)s * gridDim.x + bid) * slot_words + ((size_t)blk * NT + tid) * 2;
+      };
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          u64* d = word(slice, i * TN + j);
+          const f32x4 a = acc[i][j];
+          __hip_atomic_store(d, (u64)__float_as_uint(a[0]) | ((u64)__float_as_uint(a[1]) << 32), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+          __hip_atomic_store(d + 1, (u64)__float_as_uint(a[2]) | ((u64)__float_as_uint(a[3]) << 32), __ATOMIC_RELAXED,
+                             __HIP_MEMORY_SCOPE_SYSTEM);
+        }
+      wait_vm();  // this wave's slot stores have completed
+      __shared__ int s_last;
+      __syncthreads();
+      if (tid == 0) {
+        const int old = __hip_atomic_fetch_add(p.tile_cnt + bid, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        s_last = old == S - 1;
+        if (old == S - 1) __hip_atomic_store(p.tile_cnt + bid, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+      }
+      __syncthreads();
+      if (!s_last) return;
+      auto load = [&](int s, f32x4 (&v)[TM][TN]) {
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            if (s == slice) {
+              v[i][j] = acc[i][j];
+            } else {
+              const u64* q = word(s, i * TN + j);
+              const u64 lo = __hip_atomic_load(q, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              const u64 hi = __hip_atomic_load(q + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+              v[i][j] = f32x4{__uint_as_float((unsigned)lo), __uint_as_float((unsigned)(lo >> 32)),
+                              __uint_as_float((unsigned)hi), __uint_as_float((unsigned)(hi >> 32))};
+            }
+          }
+      };
+      // two slices per batch of loads (one memory round trip), added in order
+      f32x4 sum[TM][TN];
+      for (int s0 = 0; s0 < S; s0 += 2) {
+        f32x4 va[TM][TN], vb[TM][TN];
+        load(s0, va);
+        if (s0 + 1 < S) load(s0 + 1, vb);
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j) {
+            sum[i][j] = s0 == 0 ? va[i][j] : sum[i][j] + va[i][j];
+            if (s0 + 1 < S) sum[i][j] += vb[i][j];
+          }
+      }
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j) acc[i][j] = sum[i][j];
     }
   }
 
@@ -648,13 +734,29 @@ int store_split_slices(const GemmParams& p) {
   return (nk + per - 1) / per;  // every slice non-empty
 }
 
+// the fused split-K form (GemmParams::tile_cnt) applies: switch on, counters
+// for every tile and S slots of BM x BN fp32 per tile in `partial`
+bool fused_split(const GemmParams& p, long long tiles, int S, int BM, int BN) {
+  return knob(KNOB_SPLITK_FUSED) && p.tile_cnt && tiles <= p.tile_cnt_cap &&
+         (size_t)S * (size_t)tiles * (size_t)BM * BN <= p.slot_cap && ((uintptr_t)p.partial & 15) == 0;
+}
+
 template <int AM>
 hipError_t launch_split_store(const GemmParams& p, int S, hipStream_t st) {
+  const unsigned tiles = (unsigned)(((p.M + 63) / 64) * ((p.N + 63) / 64));
+  if (fused_split(p, tiles, S, 64, 64)) {
+    if (deep64((long long)tiles * S))
+      hipLaunchKernelGGL((gemm_kernel<64, 64, MDE_GEMM_BK, 2, 2, AM, E_STORE, 4, true>), dim3(tiles, (unsigned)S),
+                         dim3(256), 0, st, p);
+    else
+      hipLaunchKernelGGL((gemm_kernel<64, 64, MDE_GEMM_BK, 2, 2, AM, E_STORE, 0, true>), dim3(tiles, (unsigned)S),
+                         dim3(256), 0, st, p);
+    return hipGetLastError();
+  }
   GemmParams q = p;
   q.emode = E_PARTIAL;
   q.x32 = p.partial;
   q.ldo = p.N;
-  const unsigned tiles = (unsigned)(((p.M + 63) / 64) * ((p.N + 63) / 64));
   if (deep64((long long)tiles * S))
     hipLaunchKernelGGL((gemm_kernel<64, 64, MDE_GEMM_BK, 2, 2, AM, E_PARTIAL, 4>), dim3(tiles, (unsigned)S), dim3(256),
                        0, st, q);
@@ -719,6 +821,25 @@ hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
     }
     const int per = (nk + S - 1) / S;
     S = (nk + per - 1) / per;  // every slice non-empty
+    const long long t64 = (long long)((p.M + 63) / 64) * ((p.N + 63) / 64);
+    if (fused_split(p, big ? t128 : t64, S, big ? 128 : 64, big ? 128 : 64)) {
+      // one launch: the slices' tails add the slots and run the E_RESID
+      // epilogue (LN partials included) on the tile's last slice
+      if (big && w8small(t128 * S)) {
+        hipLaunchKernelGGL((gemm_kernel<128, 128, MDE_GEMM_BK, 2, 4, A_DENSE, E_RESID, 0, true>),
+                           dim3((unsigned)t128, (unsigned)S), dim3(512), 0, st, p);
+      } else if (big) {
+        hipLaunchKernelGGL((gemm_kernel<128, 128, MDE_GEMM_BK, 2, 2, A_DENSE, E_RESID, 0, true>),
+                           dim3((unsigned)t128, (unsigned)S), dim3(256), 0, st, p);
+      } else if (deep64(t64 * S)) {
+        hipLaunchKernelGGL((gemm_kernel<64, 64, MDE_GEMM_BK, 2, 2, A_DENSE, E_RESID, 4, true>), dim3((unsigned)t64, (unsigned)S),
+                           dim3(256), 0, st, p);
+      } else {
+        hipLaunchKernelGGL((gemm_kernel<64, 64, MDE_GEMM_BK, 2, 2, A_DENSE, E_RESID, 0, true>), dim3((unsigned)t64, (unsigned)S),
+                           dim3(256), 0, st, p);
+      }
+      return hipGetLastError();
+    }
     GemmParams q = p;
     q.emode = E_PARTIAL;
     q.x32 = p.partial;

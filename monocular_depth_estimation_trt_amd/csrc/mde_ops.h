@@ -71,6 +71,13 @@ struct GemmParams {
   // partial_cap > 0 the launcher picks the slice count itself, bounded by
   // partial_cap fp32 elements of `partial`
   size_t partial_cap = 0;
+  // Fused split-K (switch "splitk_fused"): with tile_cnt set (tile_cnt_cap
+  // zero-initialised arrival counters, left zero by every launch) both split
+  // paths above run as ONE launch whose last-arriving slice per tile adds the
+  // slices' slots -- S x tiles x BM x BN fp32 in `partial`, at most slot_cap
+  // elements -- in slice order and runs the epilogue; otherwise, or when the
+  // slots do not fit, the slices + reduce-kernel form
+  int* tile_cnt = nullptr; int tile_cnt_cap = 0; size_t slot_cap = 0;
   // LayerNorm folded across a GEMM boundary (DA-V2 f16-residual engines):
   //  * producer (E_RESID / E_PATCH over xh, and the split-K reduce): lnst_out
   //    = fp32 [lnst_ns][lnst_rows][2] -- per 32-column slice and token row

@@ -55,6 +55,12 @@ enum Knob : int {
   // v_mfma_f32_16x16x32_f16 (attn16_fwd_kernel; 1: on; 0: the 32x32x16
   // attn_fwd_kernel).  test_attention_16x16_matches
   KNOB_ATTN16,
+  // the split-K slices and their reduce as one launch (GemmParams::tile_cnt:
+  // the last slice of a tile to arrive adds the slots in slice order and runs
+  // the epilogue; 1: on; 0, the default: slices + splitk_resid / splitk_store
+  // kernels -- the fused tail's system-scope round trips measured slower,
+  // ViT-L B=1 3.17 -> 3.79 ms).  test_splitk_fused_matches_two_kernel
+  KNOB_SPLITK_FUSED,
   KNOB_COUNT
 };
 

@@ -167,8 +167,8 @@ size_t plan_arena_vggt(const mde_engine& e, int B, VGBuf* b, uint8_t* base) {
   t.p2 = a.h(n * s1 * F);
   t.c1 = a.h(n * s0 * (F / 2));
   t.ws_rows = n * T <= 4096 ? n * T : 0;
-  t.ws = t.ws_rows ? a.f(4 * t.ws_rows * D) : nullptr;
-  t.sws = a.f(kSplitWsFloats);
+  t.ws = t.ws_rows ? a.f(fc2_ws_floats(t.ws_rows, D)) : nullptr;
+  t.sws = a.f(kSplitWsAlloc);
   if (b) *b = t;
   return a.off;
 }
@@ -246,6 +246,9 @@ void Runner::vggt_block(const std::string& p, float eps, bool qk, int seqs, int 
     if (v.ws && (size_t)rows <= v.ws_rows && t64 < 512 && mlp >= 1024 && knob(KNOB_SPLITK)) {
       g.partial = v.ws;
       g.splitk = t64 < 256 ? 4 : 2;
+      g.slot_cap = fc2_ws_floats(rows, D);
+      g.tile_cnt = split_counters(v.sws);
+      g.tile_cnt_cap = kTileCnt;
     }
     gemm((p + "fc2").c_str(), g);
   }

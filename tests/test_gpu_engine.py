@@ -293,6 +293,40 @@ def test_fc2_splitk_matches_unsplit(gpu, encoder, size):
     assert m["max_abs"] < 0.08 and m["rel_mean"] < 1.5e-3, m
 
 
+@pytest.mark.parametrize("encoder,size", [("vitl", 518), ("vits", 98)])
+def test_splitk_fused_matches_two_kernel(gpu, encoder, size):
+    """Switch "splitk_fused" (gemm.hip gemm_kernel SPLIT): the engines' split-K
+    GEMMs -- fc2 (E_RESID, ViT-L B=1: 88 128^2 tiles x 4 slices; ViT-S 98^2:
+    64^2 tiles) and the DPT's split convs (E_STORE) -- run as ONE launch whose
+    last-arriving slice per tile adds the slots in slice order, instead of the
+    slices + splitk_resid / splitk_store.  The slice sums are the same fp32
+    additions in the same order; only the folded-LN partials of the fc2 rows
+    are grouped differently (8 columns per lane instead of 4), so the depth
+    maps agree to f16 noise, replays are bit-identical (the arrival counters
+    are re-zeroed by every launch) and the fused path meets the oracle bars.
+    Off by default: its slots and counters go through system-scope accesses
+    (the slices of a tile sit on different XCDs), and those round trips cost
+    more than the reduce launch they replace (ViT-L B=1 3.17 -> 3.79 ms,
+    gpurun_out r6f1)."""
+    from oracle import dav2_ref
+    cfg = weights.model_config(encoder, "metric")
+    sd = weights.synthetic_state_dict(cfg, 31)
+    blob = pack.pack_bytes(sd, cfg, size, size)
+    x = weights.synthetic_images(1, size, size, first_seed=71)
+    with _lib.tuning(splitk_fused=1):
+        y_fused = run_engine(blob, x, graph=True)
+        assert np.array_equal(y_fused, run_engine(blob, x, graph=False)), "fused split-K must be deterministic"
+        assert np.array_equal(y_fused, run_engine(blob, x, graph=True)), "a second context must see zeroed counters"
+    with _lib.tuning(splitk_fused=0):
+        y_two = run_engine(blob, x)
+    m = depth_metrics(y_fused, y_two)
+    print(f"fused vs two-kernel split-K {encoder} {size}", m)
+    assert m["rel_mean"] < 1e-3 and m["max_abs"] < 0.08 and m["corr"] > 0.99999, m
+    if encoder == "vits":
+        ref = dav2_ref.forward(dav2_ref.to_torch(sd), cfg, x).numpy()
+        check(y_fused, ref, 20.0, f"fused split-K {encoder} {size} vs oracle")
+
+
 @pytest.mark.parametrize("switch", ["deep64", "w8small"])
 def test_gemm_small_grid_variants_bit_exact(gpu, switch):
     """ViT-L 518^2 B=1 (config 3's unit) with a small-grid GEMM tiling switched
