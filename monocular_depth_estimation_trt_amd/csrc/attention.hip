@@ -517,7 +517,7 @@ constexpr int MERGE16_WAVE_B = 64 * 36 * 4;
 template <int NW, int NS>
 __global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4, 8)))
 attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16* __restrict__ vt,
-                  f16* __restrict__ o, int H, int T, int Tpad, int ldo) {
+                  f16* __restrict__ o, int H, int T, int Tpad, int ldo, int tail_last) {
   // NS > 1 (batch-1 grids): NS key groups of NW / NS query waves, as in
   // attn_fwd_kernel -- each group streams its slice of the key tiles through
   // its own ring slots, (O, m, l) merged through LDS after the loop
@@ -534,10 +534,29 @@ attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f1
   const int wave = wave_all - grp * NWQ;
   if (NW == 8 && NS == 1 && wave_all >= 4) __builtin_amdgcn_s_setprio(1);
   const int nqb = gridDim.x;
-  const int lin = xcd_remap(blockIdx.y * nqb + blockIdx.x, nqb * gridDim.y);
-  const int bh = lin / nqb;
+  // work order: XCD-remapped (bh, query block), or (tail_last, switch
+  // "attn_tail") every sequence's partial last query block dispatched after
+  // all full ones -- the grid's last, partly filled round then holds the
+  // blocks with idle query waves, which run shorter
+  const int id = blockIdx.y * nqb + blockIdx.x;
+  const int full = (nqb - 1) * (int)gridDim.y;
+  int bh, qblk;
+  if (NS == 1 && tail_last && nqb > 1 && T % BQ != 0) {
+    if (id < full) {
+      const int l = xcd_remap(id, full);
+      bh = l / (nqb - 1);
+      qblk = l - bh * (nqb - 1);
+    } else {
+      bh = xcd_remap(id - full, (int)gridDim.y);
+      qblk = nqb - 1;
+    }
+  } else {
+    const int lin = xcd_remap(id, nqb * gridDim.y);
+    bh = lin / nqb;
+    qblk = lin - bh * nqb;
+  }
   const int b = bh / H, h = bh - (bh / H) * H;
-  const int qbase = (lin - bh * nqb) * BQ + wave * QW;
+  const int qbase = qblk * BQ + wave * QW;
   const bool active = qbase < T;
   const int l15 = lane & 15, g = lane >> 4;
   const int nkt_all = (T + KT - 1) / KT;
@@ -870,7 +889,7 @@ hipError_t run_attn16(const h16* q, const h16* k, const h16* vt, h16* o, int B, 
   const int nqb = (T + BQ - 1) / BQ;
   hipLaunchKernelGGL((attn16_fwd_kernel<NW, NS>), dim3(nqb, B * H), dim3(NW * 64), 0, st, reinterpret_cast<const f16*>(q),
                      reinterpret_cast<const f16*>(k), reinterpret_cast<const f16*>(vt), reinterpret_cast<f16*>(o), H, T,
-                     Tpad, ldo);
+                     Tpad, ldo, knob(KNOB_ATTN_TAIL));
   return hipGetLastError();
 }
 

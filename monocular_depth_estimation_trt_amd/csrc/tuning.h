@@ -61,6 +61,10 @@ enum Knob : int {
   // kernels -- the fused tail's system-scope round trips measured slower,
   // ViT-L B=1 3.17 -> 3.79 ms).  test_splitk_fused_matches_two_kernel
   KNOB_SPLITK_FUSED,
+  // attn16's partial last query block of every sequence dispatched after all
+  // full blocks (1: on; 0: the XCD-remapped (sequence, block) order).  Work
+  // order only: bit-identical.  test_attention_tail_order_bit_exact
+  KNOB_ATTN_TAIL,
   KNOB_COUNT
 };
 

@@ -417,6 +417,39 @@ def test_attention_16x16_matches(gpu, cfg, B, H, T, spiky):
         assert not torch.equal(o32, o), "attn16 = 0 should launch the 32x32x16 kernel"
 
 
+@pytest.mark.parametrize("B,H,T", [(48, 6, 1370), (3, 5, 577), (2, 2, 256), (1, 1, 1)])
+def test_attention_tail_order_bit_exact(gpu, B, H, T):
+    """Switch "attn_tail" (attention.hip attn16_fwd_kernel): each sequence's
+    partial last query block dispatched after every full block instead of
+    the XCD-remapped (sequence, block) order.  Work order only -- every
+    workgroup computes the same queries the same way -- so the output is
+    bit-identical with the switch off (T % 256 == 0 and T = 1: no reorder)."""
+    from monocular_depth_estimation_trt_amd import _lib
+    g = torch.Generator().manual_seed(B * 1000 + T)  # own stream: the module's G sequence stays as it was
+    Tp = -(-T // 64) * 64
+    q = torch.randn(B * H, T, 64, generator=g) * 0.125 * 2.0 * LOG2E
+    k = torch.randn(B * H, T, 64, generator=g) * 2.0
+    v = torch.randn(B * H, T, 64, generator=g)
+    qg = torch.zeros(B * H, Tp, 64, dtype=torch.float16, device=gpu)
+    kg = torch.zeros_like(qg)
+    vtg = torch.zeros(B * H, 64, Tp, dtype=torch.float16, device=gpu)
+    qg[:, :T], kg[:, :T] = q.half().to(gpu), k.half().to(gpu)
+    vtg[:, :, vt_perm(T).to(gpu)] = v.transpose(1, 2).half().to(gpu)
+    outs = []
+    for tail in (1, 0):
+        o = torch.full((B * T, H * 64), float("nan"), dtype=torch.float16, device=gpu)
+        with _lib.tuning(attn_tail=tail):
+            op("mde_op_attention_cfg", ptr(qg), ptr(kg), ptr(vtg), ptr(o), B, H, T, Tp, H * 64, b"8m", None, 0,
+               stream())
+            torch.cuda.synchronize()
+        outs.append(o)
+    assert torch.isfinite(outs[0].float()).all(), "every query row written"
+    assert torch.equal(outs[0], outs[1]), "attn_tail changed the attention output"
+    if T > 1:
+        ref = attn_ref(q, k, v).reshape(B, H, T, 64).permute(0, 2, 1, 3).reshape(B * T, H * 64)
+        close(outs[0][:4096], ref[:4096], 2e-2, 5e-3, f"attention tail order B{B} H{H} T{T}")
+
+
 @pytest.mark.parametrize("cfg", ["8m", "8g2m"])
 def test_attention_16x16_pending_rescale(gpu, cfg):
     """attn16 scores a tile's second 32-key block before block 0's P.V; when
