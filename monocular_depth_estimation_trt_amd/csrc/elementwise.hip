@@ -144,32 +144,51 @@ __global__ void __launch_bounds__(256) patch_prep_kernel(const float* __restrict
                                                          f16* __restrict__ Xh, float* __restrict__ lnst,
                                                          const float* __restrict__ cls_st) {
   const long long np = (long long)ph * pw;
-  const long long nchunk = (long long)B * np * 84;  // 3 channels x 14 rows x 2 halves
-  // round-robin block order (see resize_kernel: the XCD-contiguous order
-  // reads exactly the input, 269 -> 155 MB, but takes 62.9 -> 68.4 us)
+  // one thread per (image, channel, image row, patch column): the row's 14
+  // pixels of that patch (56 B; consecutive threads read consecutive pixel
+  // runs, so a wave reads whole image rows) -> the patch's 16-wide kernel row
+  // (14 values + 2 zeros).  Round 6: the input is read once (155 MB at B =
+  // 48); the previous (patch, row, half) order fetched 269 MB.
+  const int rows = ph * 14;
+  const long long nchunk = (long long)B * 3 * rows * pw;
   long long id = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   if (id < nchunk) {
-    long long patch;
-    int r, b, pi;
+    int px, y, c, b;
     if (nchunk < (1LL << 31)) {  // 32-bit index split (a 64-bit divide is emulated)
-      const unsigned u = (unsigned)id, pu = u / 84u;
-      patch = pu;
-      r = (int)(u - pu * 84u);
-      b = (int)(pu / (unsigned)np);
-      pi = (int)(pu - (unsigned)b * (unsigned)np);
+      const unsigned u = (unsigned)id, q = u / (unsigned)pw;
+      px = (int)(u - q * (unsigned)pw);
+      const unsigned q2 = q / (unsigned)rows;
+      y = (int)(q - q2 * (unsigned)rows);
+      b = (int)(q2 / 3u);
+      c = (int)(q2 - (unsigned)b * 3u);
     } else {
-      patch = id / 84;
-      r = (int)(id - patch * 84);
-      b = (int)(patch / np);
-      pi = (int)(patch - (long long)b * np);
+      const long long q = id / pw;
+      px = (int)(id - q * pw);
+      const long long q2 = q / rows;
+      y = (int)(q - q2 * rows);
+      b = (int)(q2 / 3);
+      c = (int)(q2 - (long long)b * 3);
     }
-    const int c = r / 28, ky = (r % 28) >> 1, half = r & 1;
-    const int py = pi / pw, px = pi - (pi / pw) * pw;
-    const float* src = img + (((size_t)b * 3 + c) * H + py * 14 + ky) * W + px * 14 + half * 8;
-    float v[8];
+    const int py = y / 14, ky = y - py * 14;
+    const float* src = img + (((size_t)b * 3 + c) * H + y) * W + px * 14;
+    float v[16];
+    if ((W & 1) == 0) {  // 8-B aligned pixel runs
 #pragma unroll
-    for (int j = 0; j < 8; ++j) v[j] = (half * 8 + j < 14) ? src[j] : 0.0f;
-    store8(P + patch * PK + c * 224 + ky * 16 + half * 8, v);
+      for (int j = 0; j < 7; ++j) {
+        const float2 t = *reinterpret_cast<const float2*>(src + 2 * j);
+        v[2 * j] = t.x;
+        v[2 * j + 1] = t.y;
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 14; ++j) v[j] = src[j];
+    }
+    v[14] = v[15] = 0.0f;
+    PT* dst = P + ((long long)b * np + (long long)py * pw + px) * PK + c * 224 + ky * 16;
+    const float* lo = v;
+    const float* hi = v + 8;
+    store8(dst, *reinterpret_cast<const float(*)[8]>(lo));
+    store8(dst + 8, *reinterpret_cast<const float(*)[8]>(hi));
     return;
   }
   id -= nchunk;
@@ -386,7 +405,8 @@ hipError_t launch_layernorm32(const float* x, float* y, const float* g, const fl
 hipError_t launch_patch_prep(const float* img, h16* P, float* X, const float* cls_pos, int B, int H, int W, int ph,
                              int pw, int T, int D, hipStream_t st, h16* Xh, float* lnst, const float* cls_st, float* P32) {
   if (lnst && (!cls_st || (D & 31))) return hipErrorInvalidValue;
-  const long long n = (long long)B * ph * pw * 84 + (long long)B * D + (lnst ? (long long)B * (D / 16) : 0);
+  if (H < ph * 14 || W < pw * 14) return hipErrorInvalidValue;
+  const long long n = (long long)B * 3 * ph * 14 * pw + (long long)B * D + (lnst ? (long long)B * (D / 16) : 0);
   if (n <= 0) return hipSuccess;
   const dim3 grid((unsigned)((n + 255) / 256)), block(256);
   if (P32)
