@@ -547,7 +547,12 @@ attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f1
       bh = l / (nqb - 1);
       qblk = l - bh * (nqb - 1);
     } else {
-      bh = xcd_remap(id - full, (int)gridDim.y);
+      // each XCD's partial blocks in reverse head order: the heads whose
+      // full blocks it ran last come first, their K / V^T tiles still in its L2
+      const int u = id - full, nh = (int)gridDim.y, x = u & 7, q8 = nh >> 3, r8 = nh & 7;
+      const int size = q8 + (x < r8 ? 1 : 0);
+      const int start = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
+      bh = start + size - 1 - (u >> 3);
       qblk = nqb - 1;
     }
   } else {
