@@ -110,9 +110,10 @@ const char* mde_last_error(void);
  * split-K + reduce; "attn16" (0-1, 1) the large-grid attention on 16x16x32
  * MFMAs (same softmax, other summation grouping); "splitk_fused" (0-1, 0) the
  * engines' split-K slices and their in-order reduce as one launch (the last
- * slice of a tile to arrive adds the slots; measured slower); "attn_tail" (0-1, 1)
+ * slice of a tile to arrive adds the slots; measured slower); "attn_tail" (0-2, 2)
  * the large-grid attention's partial query blocks dispatched after the full
- * ones (work order only, bit-identical).  The environment variable of a switch is exactly
+ * ones (1: work order only, bit-identical; 2: those blocks also split their
+ * keys over two wave groups).  The environment variable of a switch is exactly
  * MDE_ + its name upper-cased (MDE_DEEP64, MDE_W8SMALL, ...); a value that is
  * not an integer in range is reported on stderr and ignored.
  * Every setting computes the same depth map within the stated tolerance; the

@@ -514,52 +514,33 @@ MDE_DEV float grp4_max(float x) {  // max over lanes (l & 15) + 16 g, g = 0..3
 // Per-lane floats one wave of a key group > 0 parks for the merge: O^T (32), m (2), l (2)
 constexpr int MERGE16_WAVE_B = 64 * 36 * 4;
 
+// LDS of the body below: the K / V^T ring, or (key groups) the merge area
 template <int NW, int NS>
-__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4, 8)))
-attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16* __restrict__ vt,
-                  f16* __restrict__ o, int H, int T, int Tpad, int ldo, int tail_last) {
-  // NS > 1 (batch-1 grids): NS key groups of NW / NS query waves, as in
-  // attn_fwd_kernel -- each group streams its slice of the key tiles through
-  // its own ring slots, (O, m, l) merged through LDS after the loop
+constexpr int attn16_smem() {
+  constexpr int NWQ = NW / NS;
+  constexpr int RING_B = 2 * NS * SLOT, MERGE_B = (NS - 1) * NWQ * MERGE16_WAVE_B;
+  return RING_B > MERGE_B ? RING_B : MERGE_B;
+}
+
+// One workgroup's queries [qblk * BQ, +BQ) of sequence x head bh (the
+// kernel below picks bh / qblk).
+// NS > 1 (batch-1 grids, and the partial blocks of attn_tail = 2): NS key
+// groups of NW / NS query waves, as in attn_fwd_kernel -- each group streams
+// its slice of the key tiles through its own ring slots, (O, m, l) merged
+// through LDS after the loop
+template <int NW, int NS>
+MDE_DEV void attn16_body(const f16* __restrict__ q, const f16* __restrict__ k, const f16* __restrict__ vt,
+                         f16* __restrict__ o, int H, int T, int Tpad, int ldo, char* smem, int bh, int qblk) {
   constexpr int NWQ = NW / NS;  // query waves per key group
   static_assert(NWQ * NS == NW && (NWQ == 2 || NWQ == 4 || NWQ == 8) && (NW == 4 || NW == 8), "waves");
   constexpr int BQ = QW * NWQ;
   constexpr int INS = 8 / NWQ;  // glds row groups per wave per 64-row image
-  constexpr int RING_B = 2 * NS * SLOT, MERGE_B = (NS - 1) * NWQ * MERGE16_WAVE_B;
-  __shared__ __attribute__((aligned(16))) char smem[RING_B > MERGE_B ? RING_B : MERGE_B];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave_all = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int grp = NS > 1 ? wave_all / NWQ : 0;
   const int wave = wave_all - grp * NWQ;
   if (NW == 8 && NS == 1 && wave_all >= 4) __builtin_amdgcn_s_setprio(1);
-  const int nqb = gridDim.x;
-  // work order: XCD-remapped (bh, query block), or (tail_last, switch
-  // "attn_tail") every sequence's partial last query block dispatched after
-  // all full ones -- the grid's last, partly filled round then holds the
-  // blocks with idle query waves, which run shorter
-  const int id = blockIdx.y * nqb + blockIdx.x;
-  const int full = (nqb - 1) * (int)gridDim.y;
-  int bh, qblk;
-  if (NS == 1 && tail_last && nqb > 1 && T % BQ != 0) {
-    if (id < full) {
-      const int l = xcd_remap(id, full);
-      bh = l / (nqb - 1);
-      qblk = l - bh * (nqb - 1);
-    } else {
-      // each XCD's partial blocks in reverse head order: the heads whose
-      // full blocks it ran last come first, their K / V^T tiles still in its L2
-      const int u = id - full, nh = (int)gridDim.y, x = u & 7, q8 = nh >> 3, r8 = nh & 7;
-      const int size = q8 + (x < r8 ? 1 : 0);
-      const int start = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
-      bh = start + size - 1 - (u >> 3);
-      qblk = nqb - 1;
-    }
-  } else {
-    const int lin = xcd_remap(id, nqb * gridDim.y);
-    bh = lin / nqb;
-    qblk = lin - bh * nqb;
-  }
   const int b = bh / H, h = bh - (bh / H) * H;
   const int qbase = qblk * BQ + wave * QW;
   const bool active = qbase < T;
@@ -803,6 +784,53 @@ attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f1
             make_uint4(sx[0], sy[0], sx[1], sy[1]);
     }
   }
+}
+
+template <int NW, int NS>
+__global__ void __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(4, 8)))
+attn16_fwd_kernel(const f16* __restrict__ q, const f16* __restrict__ k, const f16* __restrict__ vt,
+                  f16* __restrict__ o, int H, int T, int Tpad, int ldo, int tail_last) {
+  // attn_tail = 2 (8 waves, unsplit): a partial last block of at most 128
+  // queries runs as two key groups of 4 query waves (the <8, 2> body) instead
+  // of 3 active waves of 8 over all keys
+  constexpr bool KTAIL = NW == 8 && NS == 1;
+  constexpr int SM0 = attn16_smem<NW, NS>(), SM1 = KTAIL ? attn16_smem<8, 2>() : 0;
+  __shared__ __attribute__((aligned(16))) char smem[SM0 > SM1 ? SM0 : SM1];
+  constexpr int BQ = QW * (NW / NS);
+  const int nqb = gridDim.x;
+  // work order: XCD-remapped (bh, query block), or (tail_last, switch
+  // "attn_tail") every sequence's partial last query block dispatched after
+  // all full ones -- the grid's last, partly filled round then holds the
+  // blocks with idle query waves, which run shorter
+  const int id = blockIdx.y * nqb + blockIdx.x;
+  const int full = (nqb - 1) * (int)gridDim.y;
+  int bh, qblk;
+  if (NS == 1 && tail_last && nqb > 1 && T % BQ != 0) {
+    if (id < full) {
+      const int l = xcd_remap(id, full);
+      bh = l / (nqb - 1);
+      qblk = l - bh * (nqb - 1);
+    } else {
+      // each XCD's partial blocks in reverse head order: the heads whose
+      // full blocks it ran last come first, their K / V^T tiles still in its L2
+      const int u = id - full, nh = (int)gridDim.y, x = u & 7, q8 = nh >> 3, r8 = nh & 7;
+      const int size = q8 + (x < r8 ? 1 : 0);
+      const int start = x < r8 ? x * (q8 + 1) : r8 * (q8 + 1) + (x - r8) * q8;
+      bh = start + size - 1 - (u >> 3);
+      qblk = nqb - 1;
+    }
+  } else {
+    const int lin = xcd_remap(id, nqb * gridDim.y);
+    bh = lin / nqb;
+    qblk = lin - bh * nqb;
+  }
+  if constexpr (KTAIL) {
+    if (tail_last == 2 && qblk == nqb - 1 && T - qblk * BQ <= BQ / 2 && (T + KT - 1) / KT >= 2) {
+      attn16_body<8, 2>(q, k, vt, o, H, T, Tpad, ldo, smem, bh, qblk * 2);
+      return;
+    }
+  }
+  attn16_body<NW, NS>(q, k, vt, o, H, T, Tpad, ldo, smem, bh, qblk);
 }
 
 // Merge S split-KV partials: one thread per (sequence*head, query, 8 dims).

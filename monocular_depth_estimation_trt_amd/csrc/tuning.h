@@ -62,8 +62,10 @@ enum Knob : int {
   // ViT-L B=1 3.17 -> 3.79 ms).  test_splitk_fused_matches_two_kernel
   KNOB_SPLITK_FUSED,
   // attn16's partial last query block of every sequence dispatched after all
-  // full blocks (1: on; 0: the XCD-remapped (sequence, block) order).  Work
-  // order only: bit-identical.  test_attention_tail_order_bit_exact
+  // full blocks (1: work order only, bit-identical; 2, the default: and a
+  // partial block of <= 128 queries run as two key groups of 4 query waves;
+  // 0: the XCD-remapped (sequence, block) order).
+  // test_attention_tail_order_bit_exact
   KNOB_ATTN_TAIL,
   KNOB_COUNT
 };

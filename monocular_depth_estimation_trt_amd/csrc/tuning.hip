@@ -33,7 +33,7 @@ constexpr KnobDef kKnobs[KNOB_COUNT] = {
     {"narrow_resid", "MDE_NARROW_RESID", 1, 0, 1},
     {"attn16", "MDE_ATTN16", 1, 0, 1},
     {"splitk_fused", "MDE_SPLITK_FUSED", 0, 0, 1},
-    {"attn_tail", "MDE_ATTN_TAIL", 1, 0, 1},
+    {"attn_tail", "MDE_ATTN_TAIL", 2, 0, 2},
 };
 
 std::atomic<int> g_val[KNOB_COUNT];

@@ -423,7 +423,10 @@ def test_attention_tail_order_bit_exact(gpu, B, H, T):
     partial last query block dispatched after every full block instead of
     the XCD-remapped (sequence, block) order.  Work order only -- every
     workgroup computes the same queries the same way -- so the output is
-    bit-identical with the switch off (T % 256 == 0 and T = 1: no reorder)."""
+    bit-identical with the switch off (T % 256 == 0 and T = 1: no reorder).
+    attn_tail = 2 also runs a partial block of <= 128 queries as two key
+    groups of 4 query waves merged through LDS (the <8, 2> body): another
+    summation order, within 2 f16 ulp of the single-group block."""
     from monocular_depth_estimation_trt_amd import _lib
     g = torch.Generator().manual_seed(B * 1000 + T)  # own stream: the module's G sequence stays as it was
     Tp = -(-T // 64) * 64
@@ -436,7 +439,7 @@ def test_attention_tail_order_bit_exact(gpu, B, H, T):
     qg[:, :T], kg[:, :T] = q.half().to(gpu), k.half().to(gpu)
     vtg[:, :, vt_perm(T).to(gpu)] = v.transpose(1, 2).half().to(gpu)
     outs = []
-    for tail in (1, 0):
+    for tail in (1, 0, 2):
         o = torch.full((B * T, H * 64), float("nan"), dtype=torch.float16, device=gpu)
         with _lib.tuning(attn_tail=tail):
             op("mde_op_attention_cfg", ptr(qg), ptr(kg), ptr(vtg), ptr(o), B, H, T, Tp, H * 64, b"8m", None, 0,
@@ -445,6 +448,9 @@ def test_attention_tail_order_bit_exact(gpu, B, H, T):
         outs.append(o)
     assert torch.isfinite(outs[0].float()).all(), "every query row written"
     assert torch.equal(outs[0], outs[1]), "attn_tail changed the attention output"
+    assert torch.isfinite(outs[2].float()).all(), "attn_tail = 2: every query row written"
+    d = (outs[2].float() - outs[0].float()).abs().max().item()
+    assert d <= 2e-3, f"attn_tail = 2 vs 1: max |d| {d:.3g}"
     if T > 1:
         ref = attn_ref(q, k, v).reshape(B, H, T, 64).permute(0, 2, 1, 3).reshape(B * T, H * 64)
         close(outs[0][:4096], ref[:4096], 2e-2, 5e-3, f"attention tail order B{B} H{H} T{T}")
