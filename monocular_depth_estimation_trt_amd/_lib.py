@@ -248,7 +248,7 @@ def call(name: str, *args) -> None:
 
 
 TUNING = ("splitk", "lnfold", "conv_narrow", "upconv", "gemm256", "deep64", "w8small", "conv_persist", "panel",
-          "panel32", "narrow_resid", "attn16", "splitk_fused", "attn_tail")
+          "panel32", "narrow_resid", "attn16", "splitk_fused", "attn_tail", "resize_fold")
 TUNING_DEFAULT = {"panel32": 0, "splitk_fused": 0, "attn_tail": 2}  # the library's defaults where not 1 (tuning.hip kKnobs)
 
 

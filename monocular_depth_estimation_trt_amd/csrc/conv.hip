@@ -353,7 +353,7 @@ __global__ void __launch_bounds__(WM * WN * 64)
           },
           n0 + wn * TN * 16, lane, smem + wave * (TM * 16) * (TN * 16) * 4))
 #endif
-    store_tile<EM, TM, TN>(p, acc, mrow, n0 + wn * TN * 16 + (lane >> 4) * 4, lane);
+    store_tile<EM, TM, TN, true>(p, acc, mrow, n0 + wn * TN * 16 + (lane >> 4) * 4, lane);
 }
 
 template <int BN, int WM, int WN, int CK, int S, bool UP, int EM, int TY = TH>
@@ -687,19 +687,28 @@ conv64p_kernel(const GemmParams p) {
 // conv1 = ReLU'd input + bias + ReLU, conv2 = bias + residual(s), and the
 // plain conv of layer1_rn) on grids of >= 4 tiles per CU (switch "conv_persist"): ViT-S's
 // 148^2 / 74^2 RCUs at batch >= 8
-bool conv64p_launch(const GemmParams& p, hipStream_t st, hipError_t& err) {
+// conv64p mode of p (0-3, above), or -1 when the persistent conv does not take it
+int conv64p_mode(const GemmParams& p) {
   const int mode = knob(KNOB_CONV_PERSIST);
   if (!mode || p.amode != A_CONV3 || p.emode != E_STORE || p.stride != 1 || p.N != 64 || p.cc != 64 ||
       p.ch != p.oh || p.cw != p.ow || p.ldo < 64 || (p.ldo & 7) || p.res0_rows > 0)
-    return false;
+    return -1;
+  const bool r1 = p.res1 || p.res1_up;
   int m;
-  if (p.relu_in && p.act == ACT_RELU && !p.res0 && !p.res1) m = 0;
-  else if (!p.relu_in && p.act == ACT_NONE && !p.res0 && !p.res1) m = 3;
-  else if (!p.relu_in && p.act == ACT_NONE && p.res0) m = p.res1 ? 2 : 1;
-  else return false;
+  if (p.relu_in && p.act == ACT_RELU && !p.res0 && !r1) m = 0;
+  else if (!p.relu_in && p.act == ACT_NONE && !p.res0 && !r1) m = 3;
+  else if (!p.relu_in && p.act == ACT_NONE && p.res0) m = r1 ? 2 : 1;
+  else return -1;
   const int typ = mode == 2 ? 8 : 16;
   const long long tiles = (long long)p.cb * ((p.oh + typ - 1) / typ) * ((p.ow + TW - 1) / TW);
-  if (tiles < 4 * 256 || tiles >= (1ll << 31)) return false;
+  if (tiles < 4 * 256 || tiles >= (1ll << 31)) return -1;
+  return m;
+}
+
+bool conv64p_launch(const GemmParams& p, hipStream_t st, hipError_t& err) {
+  const int m = conv64p_mode(p);
+  if (m < 0) return false;
+  const int typ = knob(KNOB_CONV_PERSIST) == 2 ? 8 : 16;
   const dim3 grid(256), block(typ * 32);
   if (typ == 16) {
     if (m == 0) hipLaunchKernelGGL((conv64p_kernel<16, 0>), grid, block, 0, st, p);
@@ -1125,6 +1134,21 @@ bool conv_direct_supported(const GemmParams& p) {
   if (p.cc % 32) return false;
   if (p.amode == A_CONV3_UP) return p.stride == 1;
   return p.stride == 1 || p.stride == 2;
+}
+
+// The direct conv (conv3_kernel) reads an upsampled res1 in its epilogue
+// (GemmParams::res1_up, switch "resize_fold"): true when launch_conv3 routes
+// p there -- a stride-1 E_STORE 3x3 conv that the persistent 64-channel conv
+// does not take -- and the map has at most 64 channels.  (launch_gemm checks
+// the split-K and im2col routes first.)  ViT-S B = 1 (64 features): the
+// three resize launches gone, 0.7493 -> 0.7463 ms per forward; ViT-L B = 1's
+// 256-channel 148^2 conv paid more for the 32 gathers per pixel than the
+// launch costs (3.187 -> 3.197 ms), so wider maps keep the launch
+// (profiles/r06_resize_fold.txt).
+bool conv3_takes_res1_up(const GemmParams& p) {
+  return knob(KNOB_RESIZE_FOLD) && p.amode == A_CONV3 && p.emode == E_STORE && p.stride == 1 && p.N <= 64 &&
+         conv_direct_supported(p) && conv64p_mode(p) < 0 && p.ldo == p.N && (p.N & 7) == 0 && p.res1_uh > 0 &&
+         p.res1_uw > 0;
 }
 
 hipError_t launch_conv3(const GemmParams& p, hipStream_t st) {

@@ -327,6 +327,14 @@ __global__ void __launch_bounds__(256) resize_kernel(const f16* __restrict__ in,
     oy = (int)(pix % oh);
     b = (int)(pix / oh);
   }
+#if MDE_RESIZE_F16
+  // packed f16 blend in lerp form (mde_device.h upsample8, shared with the
+  // E_STORE epilogue's resize-on-read): each axis' two weights sum to exactly
+  // 1, so the out_conv bias folded in front of this resize (engine.hip
+  // dav2_fusion) passes unchanged and a constant map stays constant
+  // (tests/test_gpu_ops.py::test_resize_constant)
+  const f16x8 v = upsample8(in, b, ih, iw, C, oh, ow, oy, ox, c8 * 8);
+#else
   int y0, y1, x0, x1;
   float ly0, ly1, lx0, lx1;
   ac_index(ac_scale(ih, oh), oy, ih, y0, y1, ly0, ly1);
@@ -337,24 +345,6 @@ __global__ void __launch_bounds__(256) resize_kernel(const f16* __restrict__ in,
   const f16x8 c = *reinterpret_cast<const f16x8*>(base + ((size_t)y1 * iw + x0) * C);
   const f16x8 d = *reinterpret_cast<const f16x8*>(base + ((size_t)y1 * iw + x1) * C);
   f16x8 v;
-#if MDE_RESIZE_F16
-  // packed f16 blend in lerp form, a + (b - a) * w, as the up-conv staging
-  // (conv.hip): each axis' two weights sum to exactly 1, so the out_conv bias
-  // folded in front of this resize (engine.hip dav2_fusion) passes unchanged
-  // and a constant map stays constant (tests/test_gpu_ops.py::test_resize_constant)
-  typedef f16 f16x2r __attribute__((ext_vector_type(2)));
-  (void)lx0;
-  (void)ly0;
-  const f16x2r wx1 = {(f16)lx1, (f16)lx1}, wy1 = {(f16)ly1, (f16)ly1};
-#pragma unroll
-  for (int j = 0; j < 8; j += 2) {
-    const f16x2r a2 = {a[j], a[j + 1]}, b2 = {bb[j], bb[j + 1]}, c2 = {c[j], c[j + 1]}, d2 = {d[j], d[j + 1]};
-    const f16x2r t0 = a2 + (b2 - a2) * wx1, t1 = c2 + (d2 - c2) * wx1;
-    const f16x2r r = t0 + (t1 - t0) * wy1;
-    v[j] = r[0];
-    v[j + 1] = r[1];
-  }
-#else
 #pragma unroll
   for (int j = 0; j < 8; ++j)
     v[j] = (f16)(ly0 * (lx0 * (float)a[j] + lx1 * (float)bb[j]) + ly1 * (lx0 * (float)c[j] + lx1 * (float)d[j]));

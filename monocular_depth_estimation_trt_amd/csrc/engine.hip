@@ -291,12 +291,18 @@ namespace mde {
 // The 1x1 out_conv is applied BEFORE the bilinear resize (both are linear
 // and bilinear weights sum to 1, so they commute exactly in real
 // arithmetic); this runs the 1x1 GEMM on 4x fewer pixels.
-void Runner::dav2_fusion(int r, const h16* x0, const h16* x1, int B, int h, int w, h16* dst, int oh, int ow) {
+// x0_up: x0 is the x2 resize of the previous block's 1x1 output (x0_up, uh x
+// uw), not yet written -- read on the fly by rcu1's second conv (switch
+// "resize_fold"; GemmParams::res1_up), or written into x0 by that launch when
+// its conv route cannot.  Returns true when this block's own resize into dst
+// is left to the next block that way.
+bool Runner::dav2_fusion(int r, const h16* x0, const h16* x1, int B, int h, int w, h16* dst, int oh, int ow,
+                         const h16* x0_up, int uh, int uw) {
   const std::string p = "rf" + std::to_string(r);
   const int F = c.e->F;
   const h16* s = x0;
   if (x1) {
-    rcu(p + ".rcu1", x1, x0, c.b.sb, c.b.tb, B, h, w, F);
+    rcu(p + ".rcu1", x1, x0, c.b.sb, c.b.tb, B, h, w, F, false, x0_up, uh, uw);
     s = c.b.sb;
   }
   rcu(p + ".rcu2", s, nullptr, c.b.ub, c.b.tb, B, h, w, F);
@@ -306,7 +312,10 @@ void Runner::dav2_fusion(int r, const h16* x0, const h16* x1, int B, int h, int 
   g.out16 = c.b.vb;
   g.ldo = F;
   gemm((p + ".out").c_str(), g);
-  if (dst) step((p + ".resize").c_str(), [&] { return launch_resize(c.b.vb, dst, B, h, w, F, oh, ow, st); });
+  if (!dst) return false;
+  if (knob(KNOB_RESIZE_FOLD)) return true;  // vb stays intact until the next block's rcu1 has read it
+  step((p + ".resize").c_str(), [&] { return launch_resize(c.b.vb, dst, B, h, w, F, oh, ow, st); });
+  return false;
 }
 
 // The exact-fp32 DPT head (precision "fp32" packs with fp32 head weights):
@@ -723,10 +732,10 @@ hipError_t Runner::forward_dav2(int B, const void* img, float* out) {
   }
   for (int i = 0; i < 4; ++i) reassemble(i);
   // ---- fusion (refinenet4 .. refinenet1) ----
-  dav2_fusion(4, b.rn[3], nullptr, B, hs[3], ws[3], b.p4, hs[2], ws[2]);
-  dav2_fusion(3, b.p4, b.rn[2], B, hs[2], ws[2], b.p3, hs[1], ws[1]);
-  dav2_fusion(2, b.p3, b.rn[1], B, hs[1], ws[1], b.p2, hs[0], ws[0]);
-  dav2_fusion(1, b.p2, b.rn[0], B, hs[0], ws[0], nullptr, 0, 0);  // 1x1 result in vb at hs[0] x ws[0]
+  bool up = dav2_fusion(4, b.rn[3], nullptr, B, hs[3], ws[3], b.p4, hs[2], ws[2]);
+  up = dav2_fusion(3, b.p4, b.rn[2], B, hs[2], ws[2], b.p3, hs[1], ws[1], up ? b.vb : nullptr, hs[3], ws[3]);
+  up = dav2_fusion(2, b.p3, b.rn[1], B, hs[1], ws[1], b.p2, hs[0], ws[0], up ? b.vb : nullptr, hs[2], ws[2]);
+  dav2_fusion(1, b.p2, b.rn[0], B, hs[0], ws[0], nullptr, 0, 0, up ? b.vb : nullptr, hs[1], ws[1]);  // 1x1 result in vb at hs[0] x ws[0]
   // ---- head ----
   const int H1 = 2 * hs[0], W1 = 2 * ws[0];  // refinenet1 upsample x2 (fused into output_conv1's loader)
   {

@@ -360,8 +360,11 @@ struct Runner {
   // out = conv2(relu(conv1(relu(x)) + b1)) + b2 + x (+ extra)
   // relu_res: the skip adds relu(x) instead of x (an nn.ReLU(inplace=True)
   // activation overwrites the unit's input, as in VGGT's DPT head)
+  // extra_up (GemmParams::res1_up): extra is the bilinear upsample of extra_up
+  // [B][uh][uw][F], read on the fly where the conv route allows (else written
+  // into extra first)
   void rcu(const std::string& pfx, const h16* x, const h16* extra, h16* out, h16* tmp, int B, int h, int w, int F,
-           bool relu_res = false) {
+           bool relu_res = false, const h16* extra_up = nullptr, int uh = 0, int uw = 0) {
     GemmParams g1 = conv(x, B, h, w, F, pfx + ".c1.w", F, 1);
     g1.relu_in = 1;
     g1.bias = w32_opt(pfx + ".c1.b");
@@ -373,12 +376,16 @@ struct Runner {
     g2.res0 = x;
     g2.res0_relu = relu_res ? 1 : 0;
     g2.res1 = extra;
+    g2.res1_up = extra_up;
+    g2.res1_uh = uh;
+    g2.res1_uw = uw;
     g2.out16 = out;
     gemm((pfx + ".c2").c_str(), g2);
   }
 
   hipError_t forward_dav2(int B, const void* img, float* out);
-  void dav2_fusion(int r, const h16* x0, const h16* x1, int B, int h, int w, h16* dst, int oh, int ow);
+  bool dav2_fusion(int r, const h16* x0, const h16* x1, int B, int h, int w, h16* dst, int oh, int ow,
+                   const h16* x0_up = nullptr, int uh = 0, int uw = 0);
   hipError_t forward_dp(int B, const float* img, float* out, float* fov);
   void dp_encoder(const std::string& pfx, float* X, const h16* P, int nseq, int hook_seqs);
   hipError_t forward_vggt(int B, const float* img, float* out);

@@ -785,6 +785,22 @@ int gemm_store_split_slices(const GemmParams& p) { return store_split_slices(p);
 
 hipError_t launch_gemm(const GemmParams& p, hipStream_t st) {
   if (p.M <= 0 || p.N <= 0) return hipSuccess;
+  if (p.res1_up) {
+    // res1 = upsample(res1_up): read through it by the direct conv's
+    // epilogue, or written into res1 first for every other route
+    if (!p.res1 || p.amode != A_CONV3 || p.emode != E_STORE || p.res1_uh <= 0 || p.res1_uw <= 0 || (p.N & 7))
+      return hipErrorInvalidValue;
+    GemmParams q = p;
+    if (store_split_slices(p) <= 1 && !prefer_im2col(p) && conv3_takes_res1_up(p)) {
+      q.res1 = nullptr;
+      return launch_conv3(q, st);
+    }
+    const hipError_t e = launch_resize(p.res1_up, const_cast<h16*>(p.res1), p.cb, p.res1_uh, p.res1_uw, p.N, p.oh,
+                                       p.ow, st);
+    if (e != hipSuccess) return e;
+    q.res1_up = nullptr;
+    return launch_gemm(q, st);
+  }
   if (p.K <= 0 || (p.K & 7) || (p.N & 7) || (p.ldw & 63) || p.ldw < ((p.K + 63) / 64) * 64)
     return hipErrorInvalidValue;
   if (p.amode == A_DENSE && ((p.lda & 7) || p.lda < p.K)) return hipErrorInvalidValue;

@@ -97,6 +97,39 @@ MDE_DEV void ac_index(float scale, int dst, int in_size, int& i0, int& i1, float
   l0 = 1.f - l1;
 }
 
+// NHWC f16 bilinear upsample (align_corners=True) of channels [c0, c0 + 8)
+// at output pixel (oy, ox) of an oh x ow map, from in [b][ih][iw][C]: the
+// four taps blended in packed f16 in lerp form, a + (b - a) w, x then y
+// (resize_kernel, and the E_STORE epilogue's resize-on-read of
+// GemmParams::res1_up -- one function, so both give the same bits).  Each
+// axis' two weights sum to exactly 1: a constant map stays constant.
+typedef f16 f16x2u __attribute__((ext_vector_type(2)));
+MDE_DEV f16x8 upsample8(const f16* __restrict__ in, int b, int ih, int iw, int C, int oh, int ow, int oy, int ox,
+                        int c0) {
+  int y0, y1, x0, x1;
+  float ly0, ly1, lx0, lx1;
+  ac_index(ac_scale(ih, oh), oy, ih, y0, y1, ly0, ly1);
+  ac_index(ac_scale(iw, ow), ox, iw, x0, x1, lx0, lx1);
+  (void)lx0;
+  (void)ly0;
+  const f16* base = in + (size_t)b * ih * iw * C + c0;
+  const f16x8 a = *reinterpret_cast<const f16x8*>(base + ((size_t)y0 * iw + x0) * C);
+  const f16x8 bb = *reinterpret_cast<const f16x8*>(base + ((size_t)y0 * iw + x1) * C);
+  const f16x8 c = *reinterpret_cast<const f16x8*>(base + ((size_t)y1 * iw + x0) * C);
+  const f16x8 d = *reinterpret_cast<const f16x8*>(base + ((size_t)y1 * iw + x1) * C);
+  const f16x2u wx1 = {(f16)lx1, (f16)lx1}, wy1 = {(f16)ly1, (f16)ly1};
+  f16x8 v;
+#pragma unroll
+  for (int j = 0; j < 8; j += 2) {
+    const f16x2u a2 = {a[j], a[j + 1]}, b2 = {bb[j], bb[j + 1]}, c2 = {c[j], c[j + 1]}, d2 = {d[j], d[j + 1]};
+    const f16x2u t0 = a2 + (b2 - a2) * wx1, t1 = c2 + (d2 - c2) * wx1;
+    const f16x2u r = t0 + (t1 - t0) * wy1;
+    v[j] = r[0];
+    v[j + 1] = r[1];
+  }
+  return v;
+}
+
 // Storage position of key t in a V^T row: bits 2 and 3 of t swapped.  The
 // attention's P.V MFMA (32x32x16, P^T straight from the score accumulator)
 // takes, in lane half h of k-step g, the keys {16g + 4h + 0..3, 16g + 8 + 4h +

@@ -45,6 +45,12 @@ struct GemmParams {
   // ReLU residual units); res0_rows > 0 -> res0 is a table of res0_rows rows
   // repeated over m (row m % res0_rows: a per-image positional embedding)
   int res0_relu = 0; int res0_rows = 0;
+  // res1_up (switch "resize_fold"): res1 is the bilinear (align_corners)
+  // upsample of res1_up [cb][res1_uh][res1_uw][N] to the output map [cb][oh][ow]
+  // (3x3 conv problems, ldo == N).  The direct conv reads it through that
+  // upsample in its epilogue; every other path first writes the upsample into
+  // res1 (launch_gemm), so res1 must be a buffer of the output's shape either way
+  const h16* res1_up = nullptr; int res1_uh = 0, res1_uw = 0;
   float* x32 = nullptr; const float* ls = nullptr;
   // f16 residual stream: when set, E_RESID / E_PATCH update / write xh
   // [m][ldo] f16 instead of x32 (DA-V2 engines with an f16 residual)
@@ -155,6 +161,8 @@ int gemm_store_split_slices(const GemmParams& p);
 // Direct 3x3 conv with an LDS halo patch (conv.hip); launch_gemm routes
 // A_CONV3 / A_CONV3_UP problems here when conv_direct_supported().
 bool conv_direct_supported(const GemmParams& p);
+// the direct conv takes p's res1 through GemmParams::res1_up (conv.hip)
+bool conv3_takes_res1_up(const GemmParams& p);
 hipError_t launch_conv3(const GemmParams& p, hipStream_t st);
 
 // A-stationary panel GEMM (gemm_panel.hip) for K = 384 token-major E_STORE /

@@ -18,6 +18,12 @@ MDE_DEV size_t res0_offset(const GemmParams& p, int m, int n, size_t o) {
   return p.res0_rows > 0 ? (size_t)(m % p.res0_rows) * p.ldo + n : o;
 }
 
+// res1 of output row m, channels [n, n + 8), through GemmParams::res1_up
+MDE_DEV f16x8 res1_up8(const GemmParams& p, int m, int n) {
+  const int hw = p.oh * p.ow, b = m / hw, r = m - b * hw, oy = r / p.ow, ox = r - (r / p.ow) * p.ow;
+  return upsample8(reinterpret_cast<const f16*>(p.res1_up), b, p.res1_uh, p.res1_uw, p.N, p.oh, p.ow, oy, ox, n);
+}
+
 // NaN (sum, M2) for the 32-column slice of column n in row `row` of the
 // folded-LayerNorm partials (GemmParams::lnst_out)
 MDE_DEV void poison_ln_partials(const GemmParams& p, int row, int n) {
@@ -26,7 +32,8 @@ MDE_DEV void poison_ln_partials(const GemmParams& p, int row, int n) {
 }
 
 // slice: the split-K slice of an E_PARTIAL tile (its fp32 slab in x32)
-template <int EM, int TM, int TN>
+// RUP: E_STORE may read res1 through GemmParams::res1_up (the direct conv)
+template <int EM, int TM, int TN, bool RUP = false>
 MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&mrow)[TM], int ncol, int lane,
                         int slice = 0) {
   if constexpr (EM == E_HEAD) {
@@ -107,6 +114,14 @@ MDE_DEV void store_tile(const GemmParams& p, f32x4 (&acc)[TM][TN], const int (&m
             const f16x4 r1 = *reinterpret_cast<const f16x4*>(reinterpret_cast<const f16*>(p.res1) + o);
 #pragma unroll
             for (int r = 0; r < 4; ++r) v[r] += (float)r1[r];
+          }
+          if constexpr (RUP) {
+            if (p.res1_up) {
+              const f16x8 u = res1_up8(p, m, n & ~7);
+              const int hq = n & 4;
+#pragma unroll
+              for (int r = 0; r < 4; ++r) v[r] += (float)u[hq + r];
+            }
           }
           f16x4 h;
 #pragma unroll
@@ -229,7 +244,7 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
     bool f16stage = false;  // HALF: f16 rows (else fp32 in two passes)
     if constexpr (HALF) {
       bool exact = EM == E_QKV || EM == E_CONVT;
-      if constexpr (EM == E_STORE) exact = !p.res0 && !p.res1;
+      if constexpr (EM == E_STORE) exact = !p.res0 && !p.res1 && !(PRES && p.res1_up);
       f16stage = exact;
       if (!exact && (TM % 2)) return false;
     }
@@ -442,6 +457,9 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
           if constexpr (EM == E_STORE) {
             if (p.res0) pre0[it] = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res0) + res0_offset(p, m, n, o));
             if (p.res1) pre1[it] = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res1) + o);
+            if constexpr (PRES) {
+              if (p.res1_up) pre1[it] = res1_up8(p, m, n);  // (res1 itself is null then)
+            }
           } else {
             if (p.xh) pre0[it] = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.xh) + o);
           }
@@ -493,7 +511,7 @@ MDE_DEV bool store_tile_lds(const GemmParams& p, f32x4 (&acc)[TM][TN], RowMap mo
               for (int r = 0; r < 8; ++r) v[r] += (float)r0[r];
             }
           }
-          if (p.res1) {
+          if (p.res1 || (PRE && PRES && p.res1_up)) {
             f16x8 r1;
             if constexpr (PRE) r1 = pre1[it];
             else r1 = *reinterpret_cast<const f16x8*>(reinterpret_cast<const f16*>(p.res1) + o);

@@ -67,6 +67,11 @@ enum Knob : int {
   // 0: the XCD-remapped (sequence, block) order).
   // test_attention_tail_order_bit_exact
   KNOB_ATTN_TAIL,
+  // the DPT fusion blocks' x2 resize read on the fly by the next block's
+  // residual conv (GemmParams::res1_up: the direct conv's epilogue blends the
+  // four taps) instead of a resize launch (1: on).  Same bits.
+  // test_resize_fold_bit_exact
+  KNOB_RESIZE_FOLD,
   KNOB_COUNT
 };
 

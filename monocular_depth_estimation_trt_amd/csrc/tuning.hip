@@ -34,6 +34,7 @@ constexpr KnobDef kKnobs[KNOB_COUNT] = {
     {"attn16", "MDE_ATTN16", 1, 0, 1},
     {"splitk_fused", "MDE_SPLITK_FUSED", 0, 0, 1},
     {"attn_tail", "MDE_ATTN_TAIL", 2, 0, 2},
+    {"resize_fold", "MDE_RESIZE_FOLD", 1, 0, 1},
 };
 
 std::atomic<int> g_val[KNOB_COUNT];

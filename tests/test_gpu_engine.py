@@ -293,6 +293,28 @@ def test_fc2_splitk_matches_unsplit(gpu, encoder, size):
     assert m["max_abs"] < 0.08 and m["rel_mean"] < 1.5e-3, m
 
 
+@pytest.mark.parametrize("encoder,size,B", [("vits", 518, 1), ("vits", 518, 8), ("vitl", 518, 1), ("vits", 98, 2),
+                                            ("vitb", 126, 1)])
+def test_resize_fold_bit_exact(gpu, encoder, size, B):
+    """Switch "resize_fold" (engine.hip dav2_fusion, GemmParams::res1_up): the
+    fusion blocks' x2 resize is not launched; the next block's rcu1 second conv
+    reads the 1x1 output through the same align_corners blend (mde_device.h
+    upsample8) in its epilogue -- the direct conv -- or writes it into the
+    buffer first where its route is another kernel (the persistent 64-channel
+    conv at B = 8, split-K at ViT-L B = 1's 37^2 / 74^2).  The same f16
+    values reach the same adds: the depth map is bit-identical."""
+    cfg = weights.model_config(encoder, "metric")
+    sd = weights.synthetic_state_dict(cfg, 41)
+    blob = pack.pack_bytes(sd, cfg, size, size)
+    x = weights.synthetic_images(B, size, size, first_seed=13)
+    with _lib.tuning(resize_fold=1):
+        y_fold = run_engine(blob, x)
+    with _lib.tuning(resize_fold=0):
+        y_plain = run_engine(blob, x)
+    assert np.isfinite(y_fold).all()
+    assert np.array_equal(y_fold, y_plain), depth_metrics(y_fold, y_plain)
+
+
 @pytest.mark.parametrize("encoder,size", [("vitl", 518), ("vits", 98)])
 def test_splitk_fused_matches_two_kernel(gpu, encoder, size):
     """Switch "splitk_fused" (gemm.hip gemm_kernel SPLIT): the engines' split-K
