@@ -113,7 +113,8 @@ const char* mde_last_error(void);
  * slice of a tile to arrive adds the slots; measured slower); "attn_tail" (0-2, 2)
  * the large-grid attention's partial query blocks dispatched after the full
  * ones (1: work order only, bit-identical; 2: those blocks also split their
- * keys over two wave groups).  The environment variable of a switch is exactly
+ * keys over two wave groups); "resize_fold" (0-1, 1) the DPT fusion blocks' x2
+ * resize read on the fly by the next block's residual conv (bit-identical).  The environment variable of a switch is exactly
  * MDE_ + its name upper-cased (MDE_DEEP64, MDE_W8SMALL, ...); a value that is
  * not an integer in range is reported on stderr and ignored.
  * Every setting computes the same depth map within the stated tolerance; the
