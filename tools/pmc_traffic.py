@@ -72,12 +72,16 @@ def per_pass_rows(root):
 def layer_traffic(root, layer_names):
     """bytes per launch of each layer of the last forward (FETCH x2 + WRITE)."""
     fetch, write = {}, {}
+    # with "resize_fold" on there are no ".resize" steps: a fusion resize that
+    # a conv route cannot fold is launched inside the consumer conv's step,
+    # ahead of it -- count it as a helper (its bytes go to the step before)
+    helpers = HELPERS + (() if any(n.endswith(".resize") for n in layer_names) else ("resize_kernel",))
     for f, rows in per_pass_rows(root).items():
         # walk back from the end until len(layer_names) engine steps are covered
         n, i = 0, len(rows)
         while i > 0 and n < len(layer_names):
             i -= 1
-            if not any(h in rows[i][1] for h in HELPERS):
+            if not any(h in rows[i][1] for h in helpers):
                 n += 1
         if n != len(layer_names):
             raise SystemExit(f"{f}: fewer dispatches than layers")
@@ -87,7 +91,7 @@ def layer_traffic(root, layer_names):
             d, kern, cnt = fwd[j]
             vals = [cnt]
             j += 1
-            while j < len(fwd) and any(h in fwd[j][1] for h in HELPERS):
+            while j < len(fwd) and any(h in fwd[j][1] for h in helpers):
                 vals.append(fwd[j][2])
                 j += 1
             if ".attn" in name and "attn" not in kern:
